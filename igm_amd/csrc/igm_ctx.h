@@ -1,0 +1,133 @@
+// Internal context / workspace / error plumbing shared by the HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/igm_hip.h"
+
+struct igm_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // named device workspaces, grown on demand (never shrunk until destroy)
+    std::map<std::string, std::pair<void*, size_t>> ws;
+    // per kernel family: (start, stop) events of its last launch on `stream`
+    std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> kev;
+    int num_cus = 256;
+    size_t lds_per_block = 65536;
+};
+
+namespace igm {
+
+inline int fail(igm_ctx* c, int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define IGM_HIP_CHECK(ctx, expr)                                                           \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return ::igm::fail((ctx), IGM_E_HIP, "%s:%d %s -> %s", __FILE__, __LINE__,    \
+                               #expr, hipGetErrorString(_e));                              \
+    } while (0)
+
+#define IGM_TRY(expr)               \
+    do {                            \
+        int _r = (expr);            \
+        if (_r != IGM_OK) return _r; \
+    } while (0)
+
+// Device workspace slot `name` of at least `bytes` (contents undefined).
+inline int workspace(igm_ctx* c, const char* name, size_t bytes, void** out) {
+    auto& slot = c->ws[name];
+    if (slot.second < bytes) {
+        if (slot.first) {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipFree(slot.first);
+            slot.first = nullptr;
+            slot.second = 0;
+        }
+        size_t sz = bytes < 256 ? 256 : bytes;
+        if (hipMalloc(&slot.first, sz) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(c, IGM_E_NOMEM, "hipMalloc(%zu) failed for workspace '%s'", sz, name);
+        }
+        slot.second = sz;
+    }
+    *out = slot.first;
+    return IGM_OK;
+}
+
+// Get a device view of a caller array: either the pointer itself (device mode)
+// or a staged copy in workspace `name`.
+template <typename T>
+inline int to_device(igm_ctx* c, uint32_t flags, const char* name, const T* p, size_t n, const T** out) {
+    if (flags & IGM_DEVICE_PTRS || p == nullptr || n == 0) {
+        *out = p;
+        return IGM_OK;
+    }
+    void* d;
+    IGM_TRY(workspace(c, name, n * sizeof(T), &d));
+    IGM_HIP_CHECK(c, hipMemcpyAsync(d, p, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    *out = static_cast<const T*>(d);
+    return IGM_OK;
+}
+
+template <typename T>
+inline int out_device(igm_ctx* c, uint32_t flags, const char* name, T* p, size_t n, T** out) {
+    if (flags & IGM_DEVICE_PTRS || p == nullptr || n == 0) {
+        *out = p;
+        return IGM_OK;
+    }
+    void* d;
+    IGM_TRY(workspace(c, name, n * sizeof(T), &d));
+    *out = static_cast<T*>(d);
+    return IGM_OK;
+}
+
+template <typename T>
+inline int to_host(igm_ctx* c, uint32_t flags, T* host, const T* dev, size_t n) {
+    if (flags & IGM_DEVICE_PTRS || host == nullptr || n == 0 || host == dev) return IGM_OK;
+    IGM_HIP_CHECK(c, hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+    return IGM_OK;
+}
+
+inline int finish(igm_ctx* c, uint32_t flags) {
+    if (!(flags & IGM_ASYNC) || !(flags & IGM_DEVICE_PTRS)) IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    IGM_HIP_CHECK(c, hipGetLastError());
+    return IGM_OK;
+}
+
+// Event-bracketed region on the context stream (elapsed time is read lazily by
+// igm_last_kernel_ms, so timing never adds a host synchronisation).
+struct Timed {
+    igm_ctx* c;
+    std::pair<hipEvent_t, hipEvent_t>* ev;
+    Timed(igm_ctx* c_, const char* name) : c(c_) {
+        auto& e = c->kev[name];
+        if (!e.first) {
+            (void)hipEventCreate(&e.first);
+            (void)hipEventCreate(&e.second);
+        }
+        ev = &e;
+        (void)hipEventRecord(e.first, c->stream);
+    }
+    ~Timed() { (void)hipEventRecord(ev->second, c->stream); }
+};
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace igm

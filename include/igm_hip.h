@@ -1,0 +1,223 @@
+/*
+ * igm_hip.h -- C ABI of libigmhip.so, the MI355X (gfx950) engine that replaces
+ * the two hot paths of IGM (bonimba87/igm):
+ *
+ *   A-step  ActivationDistanceStep.get_actdist  (igm/steps/ActivationDistanceStep.py:336-485)
+ *           applied to every kept haploid pair   (ActivationDistanceStep.py:196-230)
+ *   M-step  serial-LAMMPS anneal + CG per structure, i.e. lammps.optimize
+ *           (igm/model/kernel/lammps.py:361-492) driven by ModelingStep.task
+ *           (igm/steps/ModelingStep.py:164-573), batched over the population.
+ *
+ * Plain C types only (no torch types).  Every entry point returns IGM_OK (0) or
+ * a negative IGM_E_* code; igm_last_error() then holds a message.  The Python
+ * shim maps a nonzero code to RuntimeError(message), which is the reference's
+ * behaviour on a failed LAMMPS run (lammps.py:453-457).
+ *
+ * Ownership: the caller owns every buffer.  With IGM_DEVICE_PTRS set in `flags`
+ * all array arguments are device pointers on the context's device (e.g. torch
+ * tensors' data_ptr()); otherwise they are host pointers and the library stages
+ * them.  Calls are stream-ordered on the context stream and return after the
+ * work has completed unless IGM_ASYNC is set (device-pointer mode only).
+ * Threading: one igm_ctx per (host thread, GPU); a context is not thread safe.
+ */
+#ifndef IGM_HIP_H
+#define IGM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IGM_OK 0
+#define IGM_E_INVALID (-1)     /* bad argument                              */
+#define IGM_E_HIP (-2)         /* HIP runtime error                         */
+#define IGM_E_NOMEM (-3)       /* device allocation failed                  */
+#define IGM_E_OVERFLOW (-4)    /* neighbour list / row capacity exceeded    */
+#define IGM_E_UNSUPPORTED (-5) /* size outside the implemented envelope      */
+
+#define IGM_DEVICE_PTRS 0x1u /* array arguments are device pointers        */
+#define IGM_ASYNC 0x2u       /* do not synchronise before returning        */
+
+typedef struct igm_ctx igm_ctx;
+
+/* ---- context ------------------------------------------------------------- */
+int igm_ctx_create(int device, igm_ctx** out);
+void igm_ctx_destroy(igm_ctx* ctx);
+const char* igm_last_error(const igm_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int igm_ctx_set_stream(igm_ctx* ctx, void* hip_stream);
+int igm_ctx_synchronize(igm_ctx* ctx);
+/* Milliseconds of the last launch of the named kernel family measured with
+ * HIP events on the context stream ("actdist", "anneal", "hic_select", ...). */
+double igm_last_kernel_ms(const igm_ctx* ctx, const char* name);
+const char* igm_version(void);
+
+/* ---- A-step: activation distances ------------------------------------------
+ * Replaces the per-pair loop ActivationDistanceStep.task (py:215-222) and
+ * get_actdist (py:336-485) over the WHOLE kept-pair list in one call, and the
+ * text round trip of task/reduce (py:228-230, 249): the emitted dist/prob are
+ * float32(float('%10.4f' % ad)) and float32(float('%.4f' % p)), bit-exact.
+ */
+typedef struct {
+    int32_t i, j;  /* haploid loci, i != j expected (i == j -> no rows)  */
+    double pwish;  /* target probability (hcs value, f32 widened)        */
+    double plast;  /* previous iteration's corrected probability         */
+} igm_pair;        /* 24 bytes: the row layout of the reference '<b>.in.npy' batches */
+
+typedef struct {
+    int32_t row, col; /* diploid bead indices                                */
+    float dist, prob; /* actdist.hdf5 {row i4, col i4, dist f4, prob f4}     */
+} igm_actdist_row;
+
+typedef struct {
+    double ad;     /* sqrt of the o-th smallest d^2 (f64), NaN if no rows */
+    double p;      /* corrected probability used (f64)                    */
+    double pnow;   /* count(d^2 <= rcut^2) / (n*S)                        */
+    int32_t o;     /* order statistic index, -1 if no rows                */
+    int32_t nrows; /* rows emitted for this pair (0, 1, 2 or 4 ...)       */
+} igm_pair_result;
+
+int igm_astep_actdist(igm_ctx* ctx, uint32_t flags,
+                      const float* xyz, /* bead-major (nbead, nstruct, 3) f32, the .hss layout */
+                      int32_t nbead, int32_t nstruct,
+                      const float* radii,     /* (nbead)                                      */
+                      const int32_t* copy_ptr, /* (nhap+1) CSR of index.copy_index             */
+                      const int32_t* copy_idx, /* diploid bead ids                             */
+                      int32_t nhap,
+                      const int32_t* chrom, /* chrom[i] as the reference indexes it (hss index.chrom) */
+                      const igm_pair* pairs, int64_t npairs,
+                      double contact_range, int32_t it_corr,
+                      igm_pair_result* per_pair,                         /* (npairs) or NULL */
+                      igm_actdist_row* rows, int64_t row_capacity,       /* CSR pair order   */
+                      int64_t* nrows_out);                               /* host pointer     */
+
+/* ---- M-step ---------------------------------------------------------------
+ * Batched replacement of lammps.optimize (lammps.py:361-492): the protocol of
+ * create_lammps_script (lammps.py:149-358) -- per stage: fix adapt of the soft
+ * prefactor, envelope scaling, optional relax run, velocity create, temp/rescale
+ * ramp, nve/limit -- followed by min_style cg.  One structure per workgroup.
+ */
+#define IGM_MAX_STAGES 16
+#define IGM_MAX_ENVELOPES 4
+
+typedef struct {
+    int32_t nstages;
+    int32_t mdsteps[IGM_MAX_STAGES];
+    double tstart[IGM_MAX_STAGES];
+    double tstop[IGM_MAX_STAGES];
+    double evfactor[IGM_MAX_STAGES];  /* fix adapt 'pair soft a' scale   */
+    double envfactor[IGM_MAX_STAGES]; /* semiaxes * envf                 */
+    int32_t relax_steps;              /* 0: no relax run                 */
+    double relax_temperature;
+    double relax_max_velocity;
+    double timestep;     /* 0.25                                       */
+    double max_velocity; /* nve/limit xmax (distance per step)         */
+    double t_window;     /* temp/rescale window (0.1)                  */
+    double t_fraction;   /* temp/rescale fraction (1.0)                */
+    double etol, ftol;   /* minimize etol ftol                         */
+    int32_t max_cg_iter, max_cg_eval;
+    double dmax;         /* min_modify dmax (LAMMPS default 0.1)       */
+    double evfactor_base;/* Steric k -> LammpsModel.evfactor           */
+    double skin;         /* neighbour skin (LAMMPS: 'neighbor maxrad') */
+    int32_t nenvelopes;
+    double env_semiaxes[IGM_MAX_ENVELOPES][3];
+    double env_k[IGM_MAX_ENVELOPES];
+    int32_t neigh_capacity; /* max neighbours per atom (0 = default)  */
+    int32_t flags;          /* reserved                                 */
+} igm_mstep_params;
+
+/* atom flags (per atom, shared by all structures of a batch) */
+#define IGM_ATOM_BEAD 0x1u   /* takes part in the soft pair potential       */
+#define IGM_ATOM_FIXED 0x2u  /* setforce 0 / not integrated (static dummy)   */
+#define IGM_ATOM_ENV0 0x10u  /* member of envelope e: IGM_ATOM_ENV0 << e     */
+
+typedef struct {
+    uint32_t i, j; /* atom indices; bit 31 of j set = harmonic_lower_bound */
+    float r0, k;   /* E = k (r - r0)^2 beyond the bound (bond_harmonic form) */
+} igm_bond;
+
+typedef struct {
+    double final_energy; /* E_pair + E_bond + sum E_env after CG ('final-energy') */
+    double pair_energy;  /* thermo epair                                        */
+    double bond_energy;  /* thermo ebond                                        */
+    double env_energy[IGM_MAX_ENVELOPES]; /* thermo f_envelope<e>               */
+    double temp;         /* thermo temp (group all)                             */
+    double einitial;     /* energy at the start of CG                           */
+    double fnorm_final;  /* |F|_2 at the end of CG                              */
+    int32_t cg_iters, cg_evals, stop_reason, nrebuild;
+} igm_opt_info;
+
+/* Run the whole protocol for `nstruct` structures of `natom` atoms each.
+ *   xyz       (nstruct, natom, 3) f32, in/out
+ *   radii     (natom) f32; atom_flags (natom)
+ *   bonds     shared bonds (polymer) + per-structure bonds (Hi-C ...):
+ *             shared_bonds[nshared]; sbond_ptr[nstruct+1] into sbonds[]
+ *   seeds     (nstruct) LAMMPS 'velocity create' seed of stage 0 (stage k: +k)
+ *   info      (nstruct) or NULL                                              */
+int igm_mstep_run(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
+                  int32_t nstruct, int32_t natom, float* xyz,
+                  const float* radii, const uint32_t* atom_flags,
+                  const igm_bond* shared_bonds, int64_t nshared,
+                  const int64_t* sbond_ptr, const igm_bond* sbonds,
+                  const int32_t* seeds, igm_opt_info* info);
+
+/* Energy/force evaluation only (parity harness for the force field):
+ * forces (nstruct, natom, 3) f32 and per-structure energies. evf/envf are the
+ * stage factors to apply.  energies: (nstruct, 3 + IGM_MAX_ENVELOPES) f64 =
+ * {total, pair, bond, env0..env3}. */
+int igm_mstep_forces(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
+                     int32_t nstruct, int32_t natom, const float* xyz,
+                     const float* radii, const uint32_t* atom_flags,
+                     const igm_bond* shared_bonds, int64_t nshared,
+                     const int64_t* sbond_ptr, const igm_bond* sbonds,
+                     double evf, double envf, float* forces, double* energies);
+
+/* Short deterministic MD segment (parity harness): `nsteps` nve/limit steps
+ * with temp/rescale ramp t0->t1 from the given velocities (no velocity create).
+ * v (nstruct, natom, 3) in/out. */
+int igm_mstep_md(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
+                 int32_t nstruct, int32_t natom, float* xyz, float* v,
+                 const float* radii, const uint32_t* atom_flags,
+                 const igm_bond* shared_bonds, int64_t nshared,
+                 const int64_t* sbond_ptr, const igm_bond* sbonds,
+                 double evf, double envf, double t0, double t1, double max_velocity,
+                 int32_t nsteps);
+
+/* ---- M-step restraint assembly: Hi-C contact selection ---------------------
+ * interHiC/intraHiC._apply (restraints/inter_hic.py:294-312, intra_hic.py) for
+ * every actdist row and every structure: a bond (i, j) is imposed when
+ * ||x_i - x_j|| <= dist (f32, no FMA) and the chromosome test holds.
+ *   xyz (nstruct, natom, 3) struct-major; act rows (n_act) from actdist.hdf5;
+ *   chrom (natom); output per-structure CSR of bonds, inter rows first then
+ *   intra rows (the reference order), r0 = cr*(r_i + r_j), k.
+ * Two-phase: call with out_bonds == NULL to get out_ptr (nstruct+1) filled and
+ * the total in *ntotal; then call again with out_bonds sized *ntotal. */
+int igm_hic_select(igm_ctx* ctx, uint32_t flags,
+                   int32_t nstruct, int32_t natom, const float* xyz,
+                   const float* radii, const int32_t* chrom,
+                   const int32_t* act_row, const int32_t* act_col, const float* act_dist,
+                   int64_t n_act, double contact_range, double kspring,
+                   int64_t* out_ptr, igm_bond* out_bonds, int64_t* ntotal);
+
+/* ---- M-step violation scoring (ModelingStep.py:511-557,859-869) ------------
+ * For each structure and each restraint class c (bond class ids 0..nclass-1 for
+ * bonds, envelope e as class nclass_bonds + e): histogram of 100 bins on [0,1]
+ * + overflow (np.histogram semantics), violated_restr, n_violations (> tol),
+ * n_imposed.  stats: (nstruct, nclass, 104) int64 =
+ * {counts[101], violated_restr, n_violations, n_imposed}.  Bond classes come
+ * from bond_class arrays parallel to shared_bonds / sbonds.  env_scale[e] is the
+ * violation scale of envelope e (0.1*mean(abc) in envelope.py:51). */
+int igm_mstep_violations(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
+                         int32_t nstruct, int32_t natom, const float* xyz,
+                         const float* radii, const uint32_t* atom_flags,
+                         const igm_bond* shared_bonds, const int32_t* shared_class, int64_t nshared,
+                         const int64_t* sbond_ptr, const igm_bond* sbonds, const int32_t* sclass,
+                         int32_t nclass_bonds, const double* env_scale, double tol,
+                         int64_t* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IGM_HIP_H */

@@ -1,0 +1,60 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (run on the GPU box with -m gpu)')
+    config.addinivalue_line('markers', 'slow: long CPU test')
+
+
+def load_golden(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+@pytest.fixture(scope='session')
+def demo_pop():
+    return load_golden('demo_population.npz')
+
+
+@pytest.fixture(scope='session')
+def demo_pairs():
+    return load_golden('demo_hic_pairs.npz')
+
+
+@pytest.fixture(scope='session')
+def g1():
+    return load_golden('actdist_golden.npz')
+
+
+@pytest.fixture(scope='session')
+def g2():
+    return load_golden('actdist_edge.npz')
+
+
+@pytest.fixture(scope='session')
+def mstep_inputs():
+    return load_golden('mstep_inputs.npz')
+
+
+def make_pairs(i, j, pwish, plast):
+    from igm_amd._lib import pair_dtype
+    a = np.zeros(len(i), pair_dtype)
+    a['i'] = i
+    a['j'] = j
+    a['pwish'] = pwish
+    a['plast'] = plast
+    return a
+
+
+def expand_per_pair(nrows, dist, prob):
+    """per-pair golden -> per-row dist/prob (rows of a pair share dist/prob)."""
+    nrows = np.asarray(nrows, np.int64)
+    return np.repeat(dist[nrows > 0], nrows[nrows > 0]), np.repeat(prob[nrows > 0], nrows[nrows > 0])
