@@ -22,6 +22,7 @@ IGM_E_OVERFLOW = -4
 IGM_E_UNSUPPORTED = -5
 IGM_DEVICE_PTRS = 0x1
 IGM_ASYNC = 0x2
+IGM_F32_PATH = 0x4
 
 IGM_MAX_STAGES = 16
 IGM_MAX_ENVELOPES = 4
@@ -98,10 +99,11 @@ SIGNATURES = {
                                 _vp, _vp, _f64, _f64, _vp, _vp]),
     'igm_mstep_md': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64,
                             _vp, _vp, _f64, _f64, _f64, _f64, _f64, _i32]),
+    'igm_velocity_create': (_i32, [_vp, _u32, _i32, _i32, _vp, _vp, _f64, _vp]),
     'igm_hic_select': (_i32, [_vp, _u32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _f64, _f64,
-                              _vp, _vp, ctypes.POINTER(_i64)]),
+                              _i32, _i32, _vp, _vp, _vp, ctypes.POINTER(_i64)]),
     'igm_mstep_violations': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp,
-                                    _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _f64, _vp]),
+                                    _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _f64, _vp]),
 }
 
 _lib = None

@@ -1,0 +1,166 @@
+// Device building blocks of the M-step engine (mstep.hip): block reductions,
+// the cell-list Verlet neighbour build, and the force field of the reference's
+// LAMMPS run (lammps.py:63-358):
+//   pair soft      E = A [1 + cos(pi r / rc)],  rc = r_i + r_j,  A = evf (rc/pi)^2
+//   bond upper/lower bound   E = K (r - r0)^2 beyond the bound (LAMMPS bond_harmonic form)
+//   ellipsoidal envelope     E = k/2 t^2, t = (1 - k2^-1/2) |x|, k2 = sum x_d^2/(s_d)^2,
+//                            s_d = envf*abc_d - r_i   (k>0: active outside; k<0: inside)
+// Every atom's force is GATHERED by the thread that owns the atom (full
+// neighbour list, both bond ends): no atomics, fixed summation order, so a run
+// is bitwise reproducible.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "igm_ctx.h"
+
+namespace igm {
+namespace ms {
+
+constexpr int kCellCap = 4096;  // cells of the per-structure binning grid
+constexpr int kMaxWaves = 16;   // 1024 threads
+
+template <typename T>
+using vec4_t = typename std::conditional<std::is_same<T, float>::value, float4, double4>::type;
+
+// protocol constants shared by every structure of a launch
+struct DevParams {
+    int nenv;
+    float env_abc[IGM_MAX_ENVELOPES][3];
+    float env_k[IGM_MAX_ENVELOPES];
+    double env_abc_d[IGM_MAX_ENVELOPES][3];
+    double env_k_d[IGM_MAX_ENVELOPES];
+    float cut_list;  // rc_max + skin
+    float skin;
+    int kcap;        // neighbour capacity per atom
+    int natom;
+    int nslice;
+};
+
+// ------------------------------------------------------------- reductions
+// Sum K doubles over the block.  Only lane 0 of each wave publishes; every
+// thread then adds the per-wave partials in the same order, so all threads get
+// the bitwise identical result (uniform control flow afterwards).  `red` must
+// not be rewritten by any thread before all threads have read it: callers
+// alternate two buffers or place a barrier.
+template <int NT, int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[w * K + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NT / 64; ++i) s += red[i * K + k];
+        v[k] = s;
+    }
+}
+
+template <int NT, int K>
+__device__ __forceinline__ void block_max(double (&v)[K], double* red) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v[k] = fmax(v[k], __shfl_xor(v[k], off));
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[w * K + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double s = red[k];
+#pragma unroll
+        for (int i = 1; i < NT / 64; ++i) s = fmax(s, red[i * K + k]);
+        v[k] = s;
+    }
+}
+
+// ------------------------------------------------------------- RanPark
+// LAMMPS RanPark (Park-Miller minimal standard, Schrage): seed_n = seed*16807^n
+// mod (2^31-1).  Jump-ahead lets every thread draw its own atoms' numbers.
+__device__ __forceinline__ uint32_t mulmod_m31(uint32_t a, uint32_t b) {
+    const uint64_t x = (uint64_t)a * (uint64_t)b;  // < 2^62
+    uint64_t r = (x & 0x7fffffffull) + (x >> 31);  // Mersenne reduction
+    r = (r & 0x7fffffffull) + (r >> 31);
+    return (uint32_t)(r >= 0x7fffffffull ? r - 0x7fffffffull : r);
+}
+__device__ __forceinline__ uint32_t powmod_m31(uint32_t base, uint64_t e) {
+    uint32_t r = 1;
+    while (e) {
+        if (e & 1) r = mulmod_m31(r, base);
+        base = mulmod_m31(base, base);
+        e >>= 1;
+    }
+    return r;
+}
+// uniform() number `n` (1-based) of a RanPark seeded with `seed`
+__device__ __forceinline__ double ranpark_nth(uint32_t seed, uint64_t n) {
+    const uint32_t s = mulmod_m31(seed % 0x7fffffffu, powmod_m31(16807u, n));
+    return (1.0 / 2147483647.0) * (double)s;
+}
+
+// ------------------------------------------------------------- force field
+// one pair (soft), returns the scalar f/r multiplier; energy added if EN
+template <typename T, bool EN>
+__device__ __forceinline__ T soft_pair(T r2, T rc, T evf, double& e) {
+    if (!(r2 < rc * rc)) return T(0);
+    const T r = sqrt(r2);
+    const T inv_pi = T(0.318309886183790671537767526745);
+    const T pref = evf * rc * inv_pi;  // A * pi / rc
+    T s, c;
+    if constexpr (std::is_same<T, float>::value) {
+        // arg = pi r / rc = 2 pi * (r / (2 rc)): v_sin_f32 / v_cos_f32 take revolutions
+        const float rev = 0.5f * r / rc;
+        s = __builtin_amdgcn_sinf(rev);
+        c = __builtin_amdgcn_cosf(rev);
+    } else {
+        sincospi(r / rc, &s, &c);
+    }
+    if (EN) e += (double)(pref * rc * inv_pi) * (1.0 + (double)c);
+    return (r > T(0)) ? pref * s / r : T(0);
+}
+
+// bond (harmonic upper/lower bound); returns f/r multiplier
+template <typename T, bool EN>
+__device__ __forceinline__ T bond_term(T r2, T r0, T k, bool lower, double& e) {
+    const T r = sqrt(r2);
+    const T dr = r - r0;
+    const bool active = lower ? (dr < T(0)) : (dr > T(0));
+    if (!active) return T(0);
+    const T rk = k * dr;
+    if (EN) e += (double)rk * (double)dr;
+    return (r > T(0)) ? T(-2) * rk / r : T(0);
+}
+
+// ellipsoidal envelope on one atom; adds force, returns energy (if EN)
+template <typename T, bool EN>
+__device__ __forceinline__ void envelope_term(T x, T y, T z, T rad, T a, T b, T c, T k, T& fx, T& fy, T& fz,
+                                              double& e) {
+    const T sx = a - rad, sy = b - rad, sz = c - rad;
+    const T ix = T(1) / (sx * sx), iy = T(1) / (sy * sy), iz = T(1) / (sz * sz);
+    const T k2 = x * x * ix + y * y * iy + z * z * iz;
+    const bool active = (k > T(0)) ? (k2 > T(1)) : (k2 < T(1) && k2 > T(0));
+    if (!active) return;
+    const T rn = sqrt(x * x + y * y + z * z);
+    const T sk = sqrt(k2);
+    const T t = (T(1) - T(1) / sk) * rn;
+    const T ka = fabs(k);
+    const T A = (T(1) - T(1) / sk) / rn;
+    const T B = rn / (k2 * sk);
+    fx -= ka * t * (A * x + B * x * ix);
+    fy -= ka * t * (A * y + B * y * iy);
+    fz -= ka * t * (A * z + B * z * iz);
+    if (EN) e += 0.5 * (double)ka * (double)t * (double)t;
+}
+
+}  // namespace ms
+}  // namespace igm

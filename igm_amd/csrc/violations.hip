@@ -1,0 +1,174 @@
+// M-step violation statistics on the GPU: the per-structure record that
+// ModelingStep.task builds after the optimisation (ModelingStep.py:511-557) with
+// the violation ratios of igm/model/forces.py and get_violation_histogram
+// (ModelingStep.py:859-869).  Compiled with -ffp-contract=off: the ratios are
+// f64 expressions on f32 coordinates, restated operation by operation, so the
+// histogram bins and the (ratio > tol) counts match the reference exactly.
+#include "igm_ctx.h"
+
+namespace {
+
+constexpr int kRec = 104;  // counts[101], violated_restr, n_violations, n_imposed
+constexpr int kMaxClass = 16;
+
+// np.histogram(v, bins=100, range=(0, 1)) bin of a value in [0, 1]
+__device__ __forceinline__ int hist_bin(double v) {
+    int i = (int)(v * 100.0);  // (a - first_edge) * norm
+    if (i >= 100) i = 99;
+    if (i < 0) i = 0;
+    const double lo = (double)i * 0.01;                     // linspace(0, 1, 101)[i]
+    const double hi = (i + 1 == 100) ? 1.0 : (double)(i + 1) * 0.01;
+    if (v < lo) --i;
+    else if (v >= hi && i != 99) ++i;
+    return i;
+}
+
+__device__ __forceinline__ void record(int* h, double v, double tol) {
+    if (v > 1.0) atomicAdd(&h[100], 1);  // overflow (v > vmax)
+    else atomicAdd(&h[hist_bin(v)], 1);
+    if (v != 0.0) atomicAdd(&h[101], 1);
+    if (v > tol) atomicAdd(&h[102], 1);
+    atomicAdd(&h[103], 1);
+}
+
+__device__ __forceinline__ float norm_f32(const float* a, const float* b) {
+    const float dx = __fsub_rn(a[0], b[0]), dy = __fsub_rn(a[1], b[1]), dz = __fsub_rn(a[2], b[2]);
+    return __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+}
+
+struct VArgs {
+    int nstruct, natom, nclass_bonds, nenv;
+    const float* xyz;
+    const float* radii;
+    const uint32_t* aflags;
+    const igm_bond* shared;
+    const int32_t* shared_class;
+    int64_t nshared;
+    const int64_t* sptr;
+    const igm_bond* sbonds;
+    const int32_t* sclass;
+    double class_cr[kMaxClass];
+    double env_abc[IGM_MAX_ENVELOPES][3];
+    double env_k[IGM_MAX_ENVELOPES];
+    double env_scale[IGM_MAX_ENVELOPES];
+    double tol;
+    int64_t* stats;
+};
+
+__global__ void __launch_bounds__(256) violations_kernel(VArgs A) {
+    __shared__ int h[kMaxClass * kRec];
+    const int s = blockIdx.x, t = threadIdx.x;
+    const int ncls = A.nclass_bonds + A.nenv;
+    for (int k = t; k < ncls * kRec; k += 256) h[k] = 0;
+    __syncthreads();
+    const float* x = A.xyz + (size_t)s * A.natom * 3;
+    const int64_t b0 = A.sptr ? A.sptr[s] : 0, b1 = A.sptr ? A.sptr[s + 1] : 0;
+    const int64_t nb = A.nshared + (b1 - b0);
+    for (int64_t q = t; q < nb; q += 256) {
+        const bool sh = q < A.nshared;
+        const igm_bond bd = sh ? A.shared[q] : A.sbonds[b0 + q - A.nshared];
+        const int c = sh ? (A.shared_class ? A.shared_class[q] : 0) : (A.sclass ? A.sclass[b0 + q - A.nshared] : 0);
+        if (c < 0 || c >= A.nclass_bonds) continue;
+        const uint32_t i = bd.i, j = bd.j & 0x7fffffffu;
+        const bool lower = (bd.j >> 31) != 0u;
+        const double dist = (double)norm_f32(x + 3 * i, x + 3 * j);  // Particle.__sub__ (f32)
+        const double cr = A.class_cr[c];
+        const double d = cr > 0.0 ? cr * (double)__fadd_rn(A.radii[i], A.radii[j]) : (double)bd.r0;
+        const double k = (double)bd.k;
+        double ratio = 0.0;
+        if (d != 0.0) {
+            double score = 0.0;
+            if (!lower) score = (dist <= d) ? 0.0 : k * (dist - d);   // HarmonicUpperBound.getScore
+            else score = (dist >= d) ? 0.0 : k * (d - dist);          // HarmonicLowerBound.getScore
+            ratio = score / (k * d);
+        }
+        record(&h[c * kRec], ratio, A.tol);
+    }
+    // EllipticEnvelope.getScores (forces.py:222-247)
+    for (int e = 0; e < A.nenv; ++e) {
+        int* he = &h[(A.nclass_bonds + e) * kRec];
+        for (int a = t; a < A.natom; a += 256) {
+            if (!(A.aflags[a] & (IGM_ATOM_ENV0 << e))) continue;
+            const float* p = x + 3 * a;
+            const double r = (double)A.radii[a];
+            double acc = 0.0;
+            for (int d = 0; d < 3; ++d) {
+                const double s2 = (A.env_abc[e][d] - r) * (A.env_abc[e][d] - r);
+                const float x2 = __fmul_rn(p[d], p[d]);  // x**2 in f32
+                acc = acc + (double)x2 / s2;
+            }
+            const double k2 = sqrt(acc);
+            double tv = 0.0;
+            if (k2 > 1.0 && A.env_k[e] > 0.0) {
+                const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(p[0], p[0]), __fmul_rn(p[1], p[1])),
+                                                       __fmul_rn(p[2], p[2])));
+                tv = (1.0 - 1.0 / sqrt(k2)) * (double)nrm / A.env_scale[e];
+            } else if (k2 < 1.0 && A.env_k[e] < 0.0) {
+                tv = 1.0 - sqrt(k2);
+            }
+            record(he, tv > 0.0 ? tv : 0.0, A.tol);
+        }
+    }
+    __syncthreads();
+    for (int k = t; k < ncls * kRec; k += 256) A.stats[(size_t)s * ncls * kRec + k] = h[k];
+}
+
+}  // namespace
+
+extern "C" int igm_mstep_violations(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nstruct,
+                                    int32_t natom, const float* xyz, const float* radii, const uint32_t* atom_flags,
+                                    const igm_bond* shared_bonds, const int32_t* shared_class, int64_t nshared,
+                                    const int64_t* sbond_ptr, const igm_bond* sbonds, const int32_t* sclass,
+                                    int32_t nclass_bonds, const double* class_cr, const double* env_scale, double tol,
+                                    int64_t* stats) {
+    using namespace igm;
+    if (!c || !prm || nstruct <= 0 || natom <= 0 || !xyz || !radii || !atom_flags || !stats || nclass_bonds < 0 ||
+        nclass_bonds + prm->nenvelopes > kMaxClass || !class_cr)
+        return fail(c, IGM_E_INVALID, "igm_mstep_violations: invalid arguments");
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    VArgs A;
+    memset(&A, 0, sizeof(A));
+    A.nstruct = nstruct;
+    A.natom = natom;
+    A.nclass_bonds = nclass_bonds;
+    A.nenv = prm->nenvelopes;
+    A.nshared = nshared;
+    A.tol = tol;
+    for (int k = 0; k < nclass_bonds; ++k) A.class_cr[k] = class_cr[k];
+    for (int e = 0; e < A.nenv; ++e) {
+        for (int d = 0; d < 3; ++d) A.env_abc[e][d] = prm->env_semiaxes[e][d];
+        A.env_k[e] = prm->env_k[e];
+        A.env_scale[e] = env_scale ? env_scale[e] : 0.1 * (prm->env_semiaxes[e][0] + prm->env_semiaxes[e][1] +
+                                                             prm->env_semiaxes[e][2]) / 3.0;
+    }
+    int64_t nsb = 0;
+    if (sbond_ptr) {
+        if (flags & IGM_DEVICE_PTRS) {
+            IGM_HIP_CHECK(c, hipMemcpyAsync(&nsb, sbond_ptr + nstruct, sizeof(int64_t), hipMemcpyDeviceToHost,
+                                            c->stream));
+            IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+        } else {
+            nsb = sbond_ptr[nstruct];
+        }
+    }
+    IGM_TRY(to_device(c, flags, "vi_xyz", xyz, (size_t)nstruct * natom * 3, &A.xyz));
+    IGM_TRY(to_device(c, flags, "vi_radii", radii, (size_t)natom, &A.radii));
+    IGM_TRY(to_device(c, flags, "vi_flags", atom_flags, (size_t)natom, &A.aflags));
+    IGM_TRY(to_device(c, flags, "vi_shared", shared_bonds, (size_t)nshared, &A.shared));
+    IGM_TRY(to_device(c, flags, "vi_shcls", shared_class, shared_class ? (size_t)nshared : 0, &A.shared_class));
+    IGM_TRY(to_device(c, flags, "vi_sptr", sbond_ptr, sbond_ptr ? (size_t)nstruct + 1 : 0, &A.sptr));
+    IGM_TRY(to_device(c, flags, "vi_sbonds", sbonds, (size_t)nsb, &A.sbonds));
+    IGM_TRY(to_device(c, flags, "vi_scls", sclass, sclass ? (size_t)nsb : 0, &A.sclass));
+    if (!sbond_ptr) A.sptr = nullptr;
+    const int ncls = nclass_bonds + A.nenv;
+    int64_t* d_stats;
+    IGM_TRY(out_device(c, flags, "vi_stats", stats, (size_t)nstruct * ncls * kRec, &d_stats));
+    A.stats = d_stats;
+    {
+        Timed tm(c, "violations");
+        hipLaunchKernelGGL(violations_kernel, dim3(nstruct), dim3(256), 0, c->stream, A);
+        IGM_HIP_CHECK(c, hipGetLastError());
+    }
+    IGM_TRY(to_host(c, flags, stats, (const int64_t*)d_stats, (size_t)nstruct * ncls * kRec));
+    return finish(c, flags);
+}

@@ -38,6 +38,7 @@ extern "C" {
 
 #define IGM_DEVICE_PTRS 0x1u /* array arguments are device pointers        */
 #define IGM_ASYNC 0x2u       /* do not synchronise before returning        */
+#define IGM_F32_PATH 0x4u    /* igm_mstep_forces: use the f32 MD force path */
 
 typedef struct igm_ctx igm_ctx;
 
@@ -166,7 +167,8 @@ int igm_mstep_run(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
 /* Energy/force evaluation only (parity harness for the force field):
  * forces (nstruct, natom, 3) f32 and per-structure energies. evf/envf are the
  * stage factors to apply.  energies: (nstruct, 3 + IGM_MAX_ENVELOPES) f64 =
- * {total, pair, bond, env0..env3}. */
+ * {total, pair, bond, env0..env3}.  Default: the f64 path of the CG kernel;
+ * with IGM_F32_PATH: the f32 path of the MD kernel (energies are NaN). */
 int igm_mstep_forces(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
                      int32_t nstruct, int32_t natom, const float* xyz,
                      const float* radii, const uint32_t* atom_flags,
@@ -185,13 +187,22 @@ int igm_mstep_md(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
                  double evf, double envf, double t0, double t1, double max_velocity,
                  int32_t nsteps);
 
+/* LAMMPS 'velocity <group> create T seed' as the reference script issues it
+ * (lammps.py:322,335: dist uniform, loop all, mom yes, Park-Miller RanPark):
+ * one velocity set per seed, atoms with IGM_ATOM_FIXED get 0 (not in the
+ * 'nonfixed' group) but still consume their random numbers.  v: (nseed, natom, 3). */
+int igm_velocity_create(igm_ctx* ctx, uint32_t flags, int32_t nseed, int32_t natom,
+                        const uint32_t* atom_flags, const int32_t* seeds, double temperature,
+                        float* v);
+
 /* ---- M-step restraint assembly: Hi-C contact selection ---------------------
  * interHiC/intraHiC._apply (restraints/inter_hic.py:294-312, intra_hic.py) for
  * every actdist row and every structure: a bond (i, j) is imposed when
  * ||x_i - x_j|| <= dist (f32, no FMA) and the chromosome test holds.
  *   xyz (nstruct, natom, 3) struct-major; act rows (n_act) from actdist.hdf5;
  *   chrom (natom); output per-structure CSR of bonds, inter rows first then
- *   intra rows (the reference order), r0 = cr*(r_i + r_j), k.
+ *   intra rows (the reference order), r0 = cr*(r_i + r_j), k; out_class (may be
+ *   NULL) receives inter_class / intra_class for each bond (violation classes).
  * Two-phase: call with out_bonds == NULL to get out_ptr (nstruct+1) filled and
  * the total in *ntotal; then call again with out_bonds sized *ntotal. */
 int igm_hic_select(igm_ctx* ctx, uint32_t flags,
@@ -199,22 +210,27 @@ int igm_hic_select(igm_ctx* ctx, uint32_t flags,
                    const float* radii, const int32_t* chrom,
                    const int32_t* act_row, const int32_t* act_col, const float* act_dist,
                    int64_t n_act, double contact_range, double kspring,
-                   int64_t* out_ptr, igm_bond* out_bonds, int64_t* ntotal);
+                   int32_t inter_class, int32_t intra_class,
+                   int64_t* out_ptr, igm_bond* out_bonds, int32_t* out_class, int64_t* ntotal);
 
 /* ---- M-step violation scoring (ModelingStep.py:511-557,859-869) ------------
- * For each structure and each restraint class c (bond class ids 0..nclass-1 for
- * bonds, envelope e as class nclass_bonds + e): histogram of 100 bins on [0,1]
- * + overflow (np.histogram semantics), violated_restr, n_violations (> tol),
- * n_imposed.  stats: (nstruct, nclass, 104) int64 =
- * {counts[101], violated_restr, n_violations, n_imposed}.  Bond classes come
- * from bond_class arrays parallel to shared_bonds / sbonds.  env_scale[e] is the
- * violation scale of envelope e (0.1*mean(abc) in envelope.py:51). */
+ * For each structure and each restraint class c -- bond classes 0..nclass_bonds-1
+ * (class ids parallel to shared_bonds / sbonds), then envelope e as class
+ * nclass_bonds + e -- the ModelingStep.task record: histogram of 100 bins on
+ * [0,1] + overflow (np.histogram semantics), violated_restr (ratio != 0),
+ * n_violations (ratio > tol) and n_imposed.
+ *   bond ratio    k (r - d) / (k d) past the bound, d = class_cr[c] * f32(r_i + r_j)
+ *                 in f64 (forces.py:131-139,178-186); class_cr[c] <= 0: d = bond r0
+ *   envelope      EllipticEnvelope.getScores (forces.py:222-247) with the base
+ *                 semiaxes, scale env_scale[e] (0.1 * mean(abc), envelope.py:51)
+ * stats: (nstruct, nclass_bonds + nenvelopes, 104) int64 =
+ *        {counts[101], violated_restr, n_violations, n_imposed}. */
 int igm_mstep_violations(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
                          int32_t nstruct, int32_t natom, const float* xyz,
                          const float* radii, const uint32_t* atom_flags,
                          const igm_bond* shared_bonds, const int32_t* shared_class, int64_t nshared,
                          const int64_t* sbond_ptr, const igm_bond* sbonds, const int32_t* sclass,
-                         int32_t nclass_bonds, const double* env_scale, double tol,
+                         int32_t nclass_bonds, const double* class_cr, const double* env_scale, double tol,
                          int64_t* stats);
 
 #ifdef __cplusplus
