@@ -1,0 +1,183 @@
+"""Benchmark of the IGM hot path on MI355X: one A/M iteration per step.
+
+Metric (BASELINE.json): "M-step structures/sec + A/M iteration wall-time".
+  step      = one igm-run loop body (bin/igm-run:105-167) at fixed sigma: the Hi-C
+              A-step (actdist over the whole population) + the M-step (restraint
+              selection, full anneal + CG protocol, violation records) of every
+              structure of this rank, everything resident in HBM.
+  value     = structures completed by all ranks / wall time of a step (structures/s)
+  ms_per_step = the A/M iteration wall-time.
+Workload at N=1: BASELINE configs[1] = SURVEY 8(d) config B: 2 Mb diploid (the demo
+index, 3008 beads + 1 static dummy), 1000 structures per GPU (weak scaling: each
+rank owns its own block of 1000 structure ids), Hi-C pairs of the demo .hcs at
+sigma = 0.02, the demo annealing protocol (47 000 MD steps + CG), synthetic
+territory initial coordinates (RandomInit semantics, seeded).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
+torch.distributed.run (one process per GPU, RCCL).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=2)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--nstruct', type=int, default=1000, help='structures per GPU')
+    ap.add_argument('--sigma', type=float, default=0.02)
+    ap.add_argument('--cpu-sample', type=int, default=16, help='structures in the CPU baseline sample (0: skip)')
+    ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--protocol-scale', type=float, default=1.0,
+                    help='scale the MD step counts (only for smoke tests; the metric needs 1.0)')
+    return ap.parse_args()
+
+
+def build_inputs(args, rank):
+    from igm_amd import model as M
+    from igm_amd import synthetic as syn
+    from igm_amd._lib import pair_dtype
+    first = rank * args.nstruct
+    pop = syn.population_2mb(args.nstruct, first_sid=first)
+    atoms = M.Atoms(pop['radii'])
+    natom = atoms.n
+    xyz = np.zeros((args.nstruct, natom, 3), np.float32)
+    xyz[:, :pop['xyz'].shape[1]] = pop['xyz']
+    chrom = np.concatenate([pop['chrom'], [-1]]).astype(np.int32)
+    poly = M.polymer_bonds(pop['chrom'], pop['copy'], pop['radii'], 2.0, 1.0)
+    proto = json.loads(json.dumps(syn.DEMO_PROTOCOL))
+    if args.protocol_scale != 1.0:
+        cap = proto['custom_annealing_protocol']
+        cap['mdsteps'] = [max(1, int(round(n * args.protocol_scale))) for n in cap['mdsteps']]
+        cap['relax']['mdsteps'] = max(1, int(round(cap['relax']['mdsteps'] * args.protocol_scale)))
+    prm = M.params_from_cfg({'optimization': {'optimizer_options': proto}}, [((5500.0,) * 3, 1.0)])
+    i, j, p = syn.hic_pairs_2mb(args.sigma)
+    pairs = np.zeros(len(i), pair_dtype)
+    pairs['i'], pairs['j'], pairs['pwish'], pairs['plast'] = i, j, p, 0.0
+    return dict(pop=pop, atoms=atoms, xyz=xyz, chrom=chrom, poly=poly, prm=prm, pairs=pairs, first=first)
+
+
+def cpu_baseline(args, it, inp):
+    """The fp64 C restatement of the LAMMPS protocol (oracle/mstep_ref.c, kind
+    'port'), one structure per thread, on a bounded sample of the same workload:
+    the first `cpu_sample` structures of rank 0 from the same initial coordinates
+    and the same Hi-C restraints the GPU M-step of step 0 used."""
+    import oracle
+    from igm_amd import model as M
+    from igm_amd._lib import bond_dtype
+    n = min(args.cpu_sample, it.S_local)
+    ptr = it.hic_ptr.cpu().numpy()
+    bonds = it.hic_bonds.cpu().numpy().view(bond_dtype)
+    sptr = ptr[:n + 1].copy()
+    sb = bonds[:sptr[-1]].copy()
+    x = inp['xyz'][:n].copy()
+    seeds = M.lammps_seeds(it.seed, np.arange(n), 0)
+    t0 = time.perf_counter()
+    oracle.mstep_run(inp['prm'], x, inp['atoms'].radii, inp['atoms'].flags, inp['poly'], sptr, sb, seeds,
+                     nthreads=min(args.cpu_threads, n))
+    dt = time.perf_counter() - t0
+    return {'value': n / dt, 'unit': 'structures/s', 'cores': min(args.cpu_threads, n), 'kind': 'port',
+            'sample': '%d structures of config B (full demo protocol, same initial coordinates and Hi-C '
+                      'restraints as GPU step 0), fp64 C restatement, one structure per thread, %.1f s'
+                      % (n, dt)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    from igm_amd.pipeline import AMIteration
+    inp = build_inputs(args, rank)
+    pop = inp['pop']
+    it = AMIteration(dev, inp['xyz'], inp['atoms'], inp['chrom'], pop['copy_ptr'], pop['copy_idx'], inp['pairs'],
+                     inp['prm'], inp['poly'], first_sid=inp['first'], rank=rank, world=world)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize(dev)
+
+    cpu = None
+    if args.cpu_sample > 0 and world == 1 and rank == 0:
+        # restraints of the initial coordinates for the baseline sample (same as GPU step 0)
+        it.astep()
+        it.select()
+        torch.cuda.synchronize(dev)
+        cpu = cpu_baseline(args, it, inp)
+        it.xyz.copy_(torch.from_numpy(inp['xyz']).to(dev))
+        it.pairs.copy_(torch.from_numpy(np.ascontiguousarray(inp['pairs'][it.pair_lo:it.pair_hi]).view(np.uint8))
+                       .to(dev))
+    for _ in range(args.warmup):
+        it.step()
+    barrier()
+    anneal_ms, bytes_launch, astep_s, mstep_s = [], [], [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tm = it.step()
+        anneal_ms.append(it.ctx.kernel_ms('anneal'))
+        bytes_launch.append(it.algorithmic_anneal_bytes())
+        astep_s.append(tm['astep_s'])
+        mstep_s.append(tm['mstep_s'])
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    score = it.violation_score()
+    info = it.info_host()
+    ms_per_step = 1000.0 * dt / max(args.steps, 1)
+    total = it.S_local * world
+    value = total * args.steps / dt
+    a_ms = float(np.mean(anneal_ms)) if anneal_ms else float('nan')
+    achieved = float(np.mean(bytes_launch)) / (a_ms * 1e-3) / 1e9 if anneal_ms else 0.0
+    if rank == 0:
+        line = {
+            'metric': 'M-step structures/sec + A/M iteration wall-time, 2Mb diploid pop=1000 per GPU',
+            'value': value, 'unit': 'structures/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': ms_per_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'f32 (MD), f64 (CG, reductions)',
+            'data': 'synthetic: RandomInit territories default_rng(1000+sid), demo .hcs pairs sigma>=%g' % args.sigma,
+            'config': {'workload': 'B: 2 Mb diploid (3008 beads), Hi-C only, %d structures per GPU, demo '
+                                   'protocol%s' % (args.nstruct, '' if args.protocol_scale == 1.0 else
+                                                   ' x%g (NOT the metric)' % args.protocol_scale),
+                       'nstruct_per_gpu': it.S_local, 'nstruct_total': total, 'sigma': args.sigma,
+                       'npairs': int(it.npairs_total), 'parallelism': 'structures sharded, A-step pair-sharded'},
+            'roofline': {'bound': 'hbm', 'kernel': 'anneal_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                         'algorithmic_bytes_per_launch': float(np.mean(bytes_launch)),
+                         'avg_launch_ms': a_ms},
+            'cpu_baseline': cpu,
+            'breakdown': {'astep_ms': 1000 * float(np.mean(astep_s)), 'mstep_ms': 1000 * float(np.mean(mstep_s)),
+                          'anneal_ms': a_ms, 'cg_ms': it.ctx.kernel_ms('cg'),
+                          'actdist_ms': it.ctx.kernel_ms('actdist'), 'hic_select_ms': it.ctx.kernel_ms('hic_select'),
+                          'violations_ms': it.ctx.kernel_ms('violations'),
+                          'violation_score': score, 'median_final_energy_per_bead':
+                              float(np.median(info['final_energy'])) / inp['atoms'].nbead,
+                          'rows': int(it.nrows), 'hic_bonds_per_struct': it.nbonds / it.S_local},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

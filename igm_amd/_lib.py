@@ -93,6 +93,7 @@ SIGNATURES = {
     'igm_version': (ctypes.c_char_p, []),
     'igm_astep_actdist': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _f64, _i32,
                                  _vp, _vp, _i64, ctypes.POINTER(_i64)]),
+    'igm_astep_update_plast': (_i32, [_vp, _u32, _vp, _i64, _vp]),
     'igm_mstep_run': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp, _vp, _i64,
                              _vp, _vp, _vp, _vp]),
     'igm_mstep_forces': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp, _vp, _i64,
@@ -100,8 +101,9 @@ SIGNATURES = {
     'igm_mstep_md': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64,
                             _vp, _vp, _f64, _f64, _f64, _f64, _f64, _i32]),
     'igm_velocity_create': (_i32, [_vp, _u32, _i32, _i32, _vp, _vp, _f64, _vp]),
-    'igm_hic_select': (_i32, [_vp, _u32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _f64, _f64,
+    'igm_hic_select': (_i32, [_vp, _u32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _f64, _f64,
                               _i32, _i32, _vp, _vp, _vp, ctypes.POINTER(_i64)]),
+    'igm_population_transpose': (_i32, [_vp, _u32, _i32, _i32, _i32, _vp, _vp, _i32]),
     'igm_mstep_violations': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp,
                                     _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _f64, _vp]),
 }

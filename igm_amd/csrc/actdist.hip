@@ -15,6 +15,7 @@
 // rounds exactly like the NumPy/CPython expressions it restates.
 #include <hipcub/hipcub.hpp>
 
+#include "exact_math.h"
 #include "igm_ctx.h"
 
 namespace {
@@ -56,15 +57,7 @@ __global__ void classify_kernel(const igm_pair* __restrict__ pairs, int64_t npai
     lists[(int64_t)b * npairs + slot] = (int)q;
 }
 
-// correctly rounded double sqrt (Tuckerman test around the hardware result)
-__device__ __forceinline__ double sqrt_rn(double x) {
-    double y = sqrt(x);
-    if (!(x > 0.0) || isinf(x)) return y;
-    double ym = nextafter(y, 0.0), yp = nextafter(y, (double)INFINITY);
-    if (fma(ym, y, -x) >= 0.0) return ym;
-    if (fma(y, yp, -x) < 0.0) return yp;
-    return y;
-}
+using igm::sqrt_rn;
 
 // CPython '%.4f' % x (exact decimal rounding of the binary value, ties to even)
 // then float('...') -> nearest double of k/10^4, which IEEE division gives.
@@ -371,5 +364,39 @@ extern "C" int igm_astep_actdist(igm_ctx* c, uint32_t flags, const float* xyz, i
         IGM_HIP_CHECK(c, hipGetLastError());
         IGM_TRY(to_host(c, flags, rows, d_rows, (size_t)total));
     }
+    return finish(c, flags);
+}
+
+namespace {
+__global__ void plast_kernel(igm_pair* __restrict__ pairs, int64_t npairs, const igm_pair_result* __restrict__ res) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= npairs) return;
+    const igm_pair_result r = res[q];
+    pairs[q].plast = r.nrows > 0 ? (double)(float)round_dec4(r.p) : 0.0;
+}
+}  // namespace
+
+extern "C" int igm_astep_update_plast(igm_ctx* c, uint32_t flags, igm_pair* pairs, int64_t npairs,
+                                      const igm_pair_result* per_pair) {
+    using namespace igm;
+    if (!c || npairs < 0 || (npairs > 0 && (!pairs || !per_pair)))
+        return fail(c, IGM_E_INVALID, "igm_astep_update_plast: invalid arguments");
+    if (npairs == 0) return IGM_OK;
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    igm_pair* d_pairs;
+    const igm_pair_result* d_res;
+    if (flags & IGM_DEVICE_PTRS) {
+        d_pairs = pairs;
+    } else {
+        void* p;
+        IGM_TRY(workspace(c, "up_pairs", sizeof(igm_pair) * npairs, &p));
+        d_pairs = (igm_pair*)p;
+        IGM_HIP_CHECK(c, hipMemcpyAsync(d_pairs, pairs, sizeof(igm_pair) * npairs, hipMemcpyHostToDevice, c->stream));
+    }
+    IGM_TRY(to_device(c, flags, "up_res", per_pair, (size_t)npairs, &d_res));
+    hipLaunchKernelGGL(plast_kernel, dim3((unsigned)ceil_div(npairs, 256)), dim3(256), 0, c->stream, d_pairs, npairs,
+                       d_res);
+    IGM_HIP_CHECK(c, hipGetLastError());
+    IGM_TRY(to_host(c, flags, pairs, (const igm_pair*)d_pairs, (size_t)npairs));
     return finish(c, flags);
 }

@@ -15,6 +15,7 @@
 // bond list of each structure is in the reference's row order.
 #include <hipcub/hipcub.hpp>
 
+#include "exact_math.h"
 #include "igm_ctx.h"
 
 namespace {
@@ -28,14 +29,13 @@ __device__ __forceinline__ bool selected(const float* x, const int32_t* chrom, i
     const float dy = __fsub_rn(x[3 * i + 1], x[3 * j + 1]);
     const float dz = __fsub_rn(x[3 * i + 2], x[3 * j + 2]);
     const float d2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
-    return __fsqrt_rn(d2) <= dist;
+    return igm::sqrt_le(d2, dist);  // RN(sqrt(d2)) <= dist, exactly
 }
 
 // pass 0 (inter) / 1 (intra): count selected rows per (structure, row block)
 __global__ void __launch_bounds__(256) count_kernel(int natom, const float* __restrict__ xyz,
                                                     const int32_t* __restrict__ chrom,
-                                                    const int32_t* __restrict__ row, const int32_t* __restrict__ col,
-                                                    const float* __restrict__ dist, int64_t n_act, int nblk,
+                                                    const igm_actdist_row* __restrict__ act, int64_t n_act, int nblk,
                                                     int64_t* __restrict__ counts) {
     const int s = blockIdx.y;
     const int pass = blockIdx.z;
@@ -44,7 +44,10 @@ __global__ void __launch_bounds__(256) count_kernel(int natom, const float* __re
     int c = 0;
     for (int u = 0; u < kRowsPerBlock / 256; ++u) {
         const int64_t q = r0 + u * 256 + threadIdx.x;
-        if (q < n_act) c += selected(x, chrom, row[q], col[q], dist[q], pass);
+        if (q < n_act) {
+            const igm_actdist_row r = act[q];
+            c += selected(x, chrom, r.row, r.col, r.dist, pass);
+        }
     }
     // block sum
     __shared__ int red[4];
@@ -58,8 +61,7 @@ __global__ void __launch_bounds__(256) count_kernel(int natom, const float* __re
 // write the selected rows in order: offsets come from the scan of count_kernel
 __global__ void __launch_bounds__(256) fill_kernel(int natom, const float* __restrict__ xyz,
                                                    const float* __restrict__ radii, const int32_t* __restrict__ chrom,
-                                                   const int32_t* __restrict__ row, const int32_t* __restrict__ col,
-                                                   const float* __restrict__ dist, int64_t n_act, int nblk,
+                                                   const igm_actdist_row* __restrict__ act, int64_t n_act, int nblk,
                                                    const int64_t* __restrict__ offs, double cr, double kspring,
                                                    int inter_class, int intra_class, igm_bond* __restrict__ out,
                                                    int32_t* __restrict__ out_class) {
@@ -75,9 +77,10 @@ __global__ void __launch_bounds__(256) fill_kernel(int natom, const float* __res
         bool sel = false;
         int i = 0, j = 0;
         if (q < n_act) {
-            i = row[q];
-            j = col[q];
-            sel = selected(x, chrom, i, j, dist[q], pass);
+            const igm_actdist_row r = act[q];
+            i = r.row;
+            j = r.col;
+            sel = selected(x, chrom, i, j, r.dist, pass);
         }
         const unsigned long long m = __ballot(sel);
         const int before = __popcll(m & ((1ull << lane) - 1ull));
@@ -119,23 +122,22 @@ __global__ void ptr_kernel(int nstruct, int nblk, const int64_t* __restrict__ of
 }  // namespace
 
 extern "C" int igm_hic_select(igm_ctx* c, uint32_t flags, int32_t nstruct, int32_t natom, const float* xyz,
-                              const float* radii, const int32_t* chrom, const int32_t* act_row,
-                              const int32_t* act_col, const float* act_dist, int64_t n_act, double contact_range,
+                              const float* radii, const int32_t* chrom, const igm_actdist_row* act,
+                              int64_t n_act, double contact_range,
                               double kspring, int32_t inter_class, int32_t intra_class, int64_t* out_ptr,
                               igm_bond* out_bonds, int32_t* out_class, int64_t* ntotal) {
     using namespace igm;
     if (!c || nstruct <= 0 || natom <= 0 || !xyz || !radii || !chrom || !out_ptr || !ntotal || n_act < 0 ||
-        (n_act > 0 && (!act_row || !act_col || !act_dist)))
+        (n_act > 0 && !act))
         return fail(c, IGM_E_INVALID, "igm_hic_select: invalid arguments");
     IGM_HIP_CHECK(c, hipSetDevice(c->device));
-    const float *d_xyz, *d_radii, *d_dist;
-    const int32_t *d_chrom, *d_row, *d_col;
+    const float *d_xyz, *d_radii;
+    const int32_t* d_chrom;
+    const igm_actdist_row* d_act;
     IGM_TRY(to_device(c, flags, "hs_xyz", xyz, (size_t)nstruct * natom * 3, &d_xyz));
     IGM_TRY(to_device(c, flags, "hs_radii", radii, (size_t)natom, &d_radii));
     IGM_TRY(to_device(c, flags, "hs_chrom", chrom, (size_t)natom, &d_chrom));
-    IGM_TRY(to_device(c, flags, "hs_row", act_row, (size_t)n_act, &d_row));
-    IGM_TRY(to_device(c, flags, "hs_col", act_col, (size_t)n_act, &d_col));
-    IGM_TRY(to_device(c, flags, "hs_dist", act_dist, (size_t)n_act, &d_dist));
+    IGM_TRY(to_device(c, flags, "hs_act", act, (size_t)n_act, &d_act));
     const int nblk = (int)std::max<int64_t>(1, ceil_div(n_act, kRowsPerBlock));
     const size_t ncnt = (size_t)nstruct * 2 * nblk;
     void *p_cnt, *p_off, *p_ptr;
@@ -152,8 +154,8 @@ extern "C" int igm_hic_select(igm_ctx* c, uint32_t flags, int32_t nstruct, int32
     int64_t* d_off = (int64_t*)p_off;
     Timed tm(c, "hic_select");
     if (n_act > 0) {
-        hipLaunchKernelGGL(count_kernel, dim3(nblk, nstruct, 2), dim3(256), 0, c->stream, natom, d_xyz, d_chrom, d_row,
-                           d_col, d_dist, n_act, nblk, d_cnt);
+        hipLaunchKernelGGL(count_kernel, dim3(nblk, nstruct, 2), dim3(256), 0, c->stream, natom, d_xyz, d_chrom, d_act,
+                           n_act, nblk, d_cnt);
     } else {
         IGM_HIP_CHECK(c, hipMemsetAsync(d_cnt, 0, sizeof(int64_t) * ncnt, c->stream));
     }
@@ -177,11 +179,82 @@ extern "C" int igm_hic_select(igm_ctx* c, uint32_t flags, int32_t nstruct, int32
         IGM_TRY(out_device(c, flags, "hs_out", out_bonds, (size_t)total, &d_out));
         if (out_class) IGM_TRY(out_device(c, flags, "hs_cls", out_class, (size_t)total, &d_cls));
         hipLaunchKernelGGL(fill_kernel, dim3(nblk, nstruct, 2), dim3(256), 0, c->stream, natom, d_xyz, d_radii,
-                           d_chrom, d_row, d_col, d_dist, n_act, nblk, d_off, contact_range, kspring, inter_class,
+                           d_chrom, d_act, n_act, nblk, d_off, contact_range, kspring, inter_class,
                            intra_class, d_out, d_cls);
         IGM_HIP_CHECK(c, hipGetLastError());
         IGM_TRY(to_host(c, flags, out_bonds, d_out, (size_t)total));
         if (out_class) IGM_TRY(to_host(c, flags, out_class, d_cls, (size_t)total));
     }
+    return finish(c, flags);
+}
+
+namespace {
+// 32x32-atom tiles through LDS: both sides of the transpose are coalesced
+__global__ void __launch_bounds__(256) transpose_kernel(int nbead, int nstruct, int natom, const float* __restrict__ src,
+                                                        float* __restrict__ dst, int direction) {
+    __shared__ float tile[32][32 * 3 + 1];
+    const int b0 = blockIdx.x * 32, s0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    if (direction == 0) {  // src bead-major (nbead, nstruct, 3) -> dst (nstruct, natom, 3)
+        for (int r = ty; r < 32; r += 8) {
+            const int b = b0 + r;
+            for (int q = tx; q < 96; q += 32) {
+                const int s = s0 + q / 3;
+                if (b < nbead && s < nstruct) tile[r][q] = src[((size_t)b * nstruct + s) * 3 + q % 3];
+            }
+        }
+        __syncthreads();
+        for (int r = ty; r < 32; r += 8) {
+            const int s = s0 + r;
+            for (int q = tx; q < 96; q += 32) {
+                const int b = b0 + q / 3;
+                if (b < nbead && s < nstruct) dst[((size_t)s * natom + b) * 3 + q % 3] = tile[q / 3][r * 3 + q % 3];
+            }
+        }
+    } else {  // src struct-major (nstruct, natom, 3) -> dst bead-major (nbead, nstruct, 3)
+        for (int r = ty; r < 32; r += 8) {
+            const int s = s0 + r;
+            for (int q = tx; q < 96; q += 32) {
+                const int b = b0 + q / 3;
+                if (b < nbead && s < nstruct) tile[q / 3][r * 3 + q % 3] = src[((size_t)s * natom + b) * 3 + q % 3];
+            }
+        }
+        __syncthreads();
+        for (int r = ty; r < 32; r += 8) {
+            const int b = b0 + r;
+            for (int q = tx; q < 96; q += 32) {
+                const int s = s0 + q / 3;
+                if (b < nbead && s < nstruct) dst[((size_t)b * nstruct + s) * 3 + q % 3] = tile[r][q];
+            }
+        }
+    }
+}
+}  // namespace
+
+extern "C" int igm_population_transpose(igm_ctx* c, uint32_t flags, int32_t nbead, int32_t nstruct, int32_t natom,
+                                        const float* src, float* dst, int32_t direction) {
+    using namespace igm;
+    if (!c || nbead <= 0 || nstruct <= 0 || natom < nbead || !src || !dst || (direction != 0 && direction != 1))
+        return fail(c, IGM_E_INVALID, "igm_population_transpose: invalid arguments");
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    const size_t nsrc = direction == 0 ? (size_t)nbead * nstruct * 3 : (size_t)nstruct * natom * 3;
+    const size_t ndst = direction == 0 ? (size_t)nstruct * natom * 3 : (size_t)nbead * nstruct * 3;
+    const float* d_src;
+    float* d_dst;
+    IGM_TRY(to_device(c, flags, "tr_src", src, nsrc, &d_src));
+    if (flags & IGM_DEVICE_PTRS) {
+        d_dst = dst;
+    } else {
+        void* p;
+        IGM_TRY(workspace(c, "tr_dst", sizeof(float) * ndst, &p));
+        d_dst = (float*)p;
+        if (direction == 0)  // extra atoms keep the caller's values
+            IGM_HIP_CHECK(c, hipMemcpyAsync(d_dst, dst, sizeof(float) * ndst, hipMemcpyHostToDevice, c->stream));
+    }
+    dim3 grid((unsigned)ceil_div(nbead, 32), (unsigned)ceil_div(nstruct, 32));
+    hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, c->stream, nbead, nstruct, natom, d_src, d_dst,
+                       direction);
+    IGM_HIP_CHECK(c, hipGetLastError());
+    IGM_TRY(to_host(c, flags, dst, (const float*)d_dst, ndst));
     return finish(c, flags);
 }

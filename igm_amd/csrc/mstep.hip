@@ -21,12 +21,16 @@
 //    f64 positions in LDS, because its energy tests (EMACH = 1e-8) need it.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+#include <unordered_map>
+
 #include "mstep_common.h"
 
 namespace igm {
 namespace ms {
 
 constexpr uint32_t kLowerBit = 0x80000000u;
+constexpr int kMaxTypes = 2048;  // distinct radii (LAMMPS atom types); the pair table is kMaxTypes^2
 
 struct Bonds {
     const int4* ent;     // all structures' SELL entries
@@ -38,6 +42,7 @@ struct Bonds {
 struct Common {
     int nstruct, natom, nslice, kcap;
     const float* radii;
+    const int* atype;  // per atom: index into DevParams::pair_tab / rtype
     const uint32_t* aflags;
     Bonds bonds;
     int* work_counter;  // dynamic structure scheduler
@@ -280,7 +285,7 @@ __device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, i
 }
 
 // ------------------------------------------------------------- forces
-// force (and energy if EN) on atom a; position p0 (w = radius, <0: no pair)
+// force (and energy if EN) on atom a; position p0 (w: f32 radius / f64 atom type, <0: no pair)
 template <typename T, bool EN>
 __device__ __forceinline__ void atom_force(int a, const vec4_t<T>& p0, uint32_t fl, const vec4_t<T>* pos,
                                            const uint16_t* nl, int nn, const int4* al, int nd, const DevParams& P,
@@ -301,7 +306,13 @@ __device__ __forceinline__ void atom_force(int a, const vec4_t<T>& p0, uint32_t 
                 const vec4_t<T> p = pos[jv[u]];
                 const T dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
                 double e = 0.0;
-                const T fp = soft_pair<T, EN>(dx * dx + dy * dy + dz * dz, ri + (T)p.w, evf, e);
+                T fp;
+                if constexpr (std::is_same<T, float>::value) {
+                    fp = soft_pair<T, EN>(dx * dx + dy * dy + dz * dz, ri + (T)p.w, evf, e);
+                } else {
+                    const double2 pc = P.pair_tab[(int)ri * P.ntype + (int)p.w];
+                    fp = soft_pair_typed(dx * dx + dy * dy + dz * dz, pc.x, pc.y, evf, e);
+                }
                 fx += fp * dx;
                 fy += fp * dy;
                 fz += fp * dz;
@@ -329,7 +340,12 @@ __device__ __forceinline__ void atom_force(int a, const vec4_t<T>& p0, uint32_t 
             if (EN) eb += 0.5 * e;
         }
     }
-    const T rad = ri >= T(0) ? ri : -ri - T(1);  // non-bead atoms carry -(r + 1)
+    // non-bead atoms carry -(w + 1); f32: w = radius, f64: w = atom type
+    T rad;
+    if constexpr (std::is_same<T, float>::value)
+        rad = ri >= T(0) ? ri : -ri - T(1);
+    else
+        rad = P.rtype[ri >= T(0) ? (int)ri : (int)(-ri - T(1))];
     for (int e = 0; e < P.nenv; ++e) {
         if (!(fl & (IGM_ATOM_ENV0 << e))) continue;
         double en = 0.0;
@@ -477,7 +493,10 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                                              ee);
                     sm.frc[a] = make_float4(fx, fy, fz, 0.f);
                 }
-                if (step == 0) continue;
+                if (step == 0) {
+                    __syncthreads();  // setup forces read sm.pos: no update before every wave is done
+                    continue;
+                }
                 double ts[1] = {0.0};
 #pragma unroll
                 for (int b = 0; b < BPT; ++b) {  // final_integrate
@@ -637,7 +656,7 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
             const int a = b * NT + t;
             const bool in = a < natom;
             const uint32_t fl = in ? A.cm.aflags[a] : 0u;
-            const double r = in ? (double)A.cm.radii[a] : 0.0;
+            const double r = in ? (double)A.cm.atype[a] : 0.0;
             sm.pos[a] = make_double4(in ? (double)xs[(size_t)a * 3] : 0.0, in ? (double)xs[(size_t)a * 3 + 1] : 0.0,
                                      in ? (double)xs[(size_t)a * 3 + 2] : 0.0,
                                      (in && (fl & IGM_ATOM_BEAD)) ? r : -(r + 1.0));
@@ -1040,9 +1059,21 @@ struct Prepared {
     int64_t total_ent;
 };
 
-int make_devparams(igm_ctx* c, const igm_mstep_params* prm, int natom, const float* radii_h_or_d, uint32_t flags,
-                   const float* d_radii, const uint32_t* d_flags, DevParams* P) {
-    // max bead radius: need host copies of radii/flags
+// The reference writes np.float32 values with Python's shortest round-trip repr
+// (PairIJ cutoff and 'User' radius, lammps.py:128-146) and LAMMPS parses them as
+// doubles: the shortest %.{p}g that reads back as the same float, read as double.
+static double f32_as_printed(float f) {
+    char buf[48];
+    for (int p = 1; p <= 9; ++p) {
+        snprintf(buf, sizeof(buf), "%.*g", p, (double)f);
+        if (strtof(buf, nullptr) == f) return strtod(buf, nullptr);
+    }
+    return (double)f;
+}
+
+int make_devparams(igm_ctx* c, const igm_mstep_params* prm, int natom, const float* d_radii,
+                   const uint32_t* d_flags, DevParams* P, const int** d_atype) {
+    // host copies of radii/flags: max bead radius and the atom types
     std::vector<float> r(natom);
     std::vector<uint32_t> fl(natom);
     IGM_HIP_CHECK(c, hipMemcpyAsync(r.data(), d_radii, sizeof(float) * natom, hipMemcpyDeviceToHost, c->stream));
@@ -1067,8 +1098,43 @@ int make_devparams(igm_ctx* c, const igm_mstep_params* prm, int natom, const flo
     P->kcap = prm->neigh_capacity > 0 ? prm->neigh_capacity : 96;
     P->natom = natom;
     P->nslice = (natom + 63) / 64;
-    (void)radii_h_or_d;
-    (void)flags;
+    // atom types: one per distinct f32 radius, in order of first appearance
+    std::vector<int> type(natom);
+    std::vector<float> tr;
+    std::unordered_map<uint32_t, int> seen;
+    for (int i = 0; i < natom; ++i) {
+        uint32_t key;
+        memcpy(&key, &r[i], 4);
+        auto it = seen.find(key);
+        if (it == seen.end()) {
+            it = seen.emplace(key, (int)tr.size()).first;
+            tr.push_back(r[i]);
+        }
+        type[i] = it->second;
+    }
+    const int nt = (int)tr.size();
+    if (nt > kMaxTypes) return fail(c, IGM_E_UNSUPPORTED, "%d distinct radii (> %d atom types)", nt, kMaxTypes);
+    std::vector<double2> tab((size_t)nt * nt);
+    std::vector<double> rt(nt);
+    for (int a = 0; a < nt; ++a) {
+        rt[a] = f32_as_printed(tr[a]);
+        for (int b = 0; b < nt; ++b) {
+            const float dc = tr[a] + tr[b];
+            tab[(size_t)a * nt + b] = make_double2((double)dc, f32_as_printed(dc));
+        }
+    }
+    void *p_t, *p_tab, *p_rt;
+    IGM_TRY(workspace(c, "ms_atype", sizeof(int) * (size_t)natom, &p_t));
+    IGM_TRY(workspace(c, "ms_ptab", sizeof(double2) * tab.size(), &p_tab));
+    IGM_TRY(workspace(c, "ms_rtype", sizeof(double) * (size_t)nt, &p_rt));
+    IGM_HIP_CHECK(c, hipMemcpyAsync(p_t, type.data(), sizeof(int) * natom, hipMemcpyHostToDevice, c->stream));
+    IGM_HIP_CHECK(c, hipMemcpyAsync(p_tab, tab.data(), sizeof(double2) * tab.size(), hipMemcpyHostToDevice, c->stream));
+    IGM_HIP_CHECK(c, hipMemcpyAsync(p_rt, rt.data(), sizeof(double) * nt, hipMemcpyHostToDevice, c->stream));
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));  // host vectors die here
+    P->ntype = nt;
+    P->pair_tab = (const double2*)p_tab;
+    P->rtype = (const double*)p_rt;
+    *d_atype = (const int*)p_t;
     return IGM_OK;
 }
 
@@ -1099,7 +1165,8 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
     if (nsb == 0) d_sb = nullptr;
     if (!sbond_ptr) d_sptr = nullptr;
     DevParams P;
-    IGM_TRY(make_devparams(c, prm, natom, radii, flags, d_radii, d_flags, &P));
+    const int* d_atype;
+    IGM_TRY(make_devparams(c, prm, natom, d_radii, d_flags, &P, &d_atype));
     const int nslice = P.nslice;
     void *p_deg, *p_soff, *p_size, *p_base, *p_err, *p_wc;
     IGM_TRY(workspace(c, "ms_deg", sizeof(int) * (size_t)nstruct * natom, &p_deg));
@@ -1149,6 +1216,7 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
     out->cm.nslice = nslice;
     out->cm.kcap = P.kcap;
     out->cm.radii = d_radii;
+    out->cm.atype = d_atype;
     out->cm.aflags = d_flags;
     out->cm.bonds.base = (const int64_t*)p_base;
     out->cm.bonds.soff = (const int*)p_soff;

@@ -36,6 +36,13 @@ struct DevParams {
     int kcap;        // neighbour capacity per atom
     int natom;
     int nslice;
+    // f64 path: the reference's LAMMPS atom types (one per distinct radius,
+    // lammps.py:114-146).  pair_tab[ti*ntype+tj] = {dc = f32(ri + rj), rc = the
+    // PairIJ cutoff LAMMPS parses from repr(dc)}; rtype = repr(radius) as the
+    // 'User' data line is read.
+    int ntype;
+    const double2* pair_tab;
+    const double* rtype;
 };
 
 // ------------------------------------------------------------- reductions
@@ -127,6 +134,20 @@ __device__ __forceinline__ T soft_pair(T r2, T rc, T evf, double& e) {
     }
     if (EN) e += (double)(pref * rc * inv_pi) * (1.0 + (double)c);
     return (r > T(0)) ? pref * s / r : T(0);
+}
+
+// f64 soft pair exactly as LAMMPS evaluates the printed coefficients:
+// A = evf (dc/pi)^2 at full precision, cutoff and argument from the parsed rc
+__device__ __forceinline__ double soft_pair_typed(double r2, double dc, double rc, double evf, double& e) {
+    if (!(r2 < rc * rc)) return 0.0;
+    const double kPi = 3.14159265358979323846;
+    const double A = (dc / kPi) * (dc / kPi) * evf;
+    const double r = sqrt(r2);
+    const double arg = kPi * r / rc;
+    double s, c;
+    sincos(arg, &s, &c);
+    e += A * (1.0 + c);
+    return (r > 0.0) ? A * s * kPi / rc / r : 0.0;
 }
 
 // bond (harmonic upper/lower bound); returns f/r multiplier

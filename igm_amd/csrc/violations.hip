@@ -4,6 +4,7 @@
 // (ModelingStep.py:859-869).  Compiled with -ffp-contract=off: the ratios are
 // f64 expressions on f32 coordinates, restated operation by operation, so the
 // histogram bins and the (ratio > tol) counts match the reference exactly.
+#include "exact_math.h"
 #include "igm_ctx.h"
 
 namespace {
@@ -33,7 +34,7 @@ __device__ __forceinline__ void record(int* h, double v, double tol) {
 
 __device__ __forceinline__ float norm_f32(const float* a, const float* b) {
     const float dx = __fsub_rn(a[0], b[0]), dy = __fsub_rn(a[1], b[1]), dz = __fsub_rn(a[2], b[2]);
-    return __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+    return igm::sqrtf_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
 }
 
 struct VArgs {
@@ -97,14 +98,14 @@ __global__ void __launch_bounds__(256) violations_kernel(VArgs A) {
                 const float x2 = __fmul_rn(p[d], p[d]);  // x**2 in f32
                 acc = acc + (double)x2 / s2;
             }
-            const double k2 = sqrt(acc);
+            const double k2 = igm::sqrt_rn(acc);
             double tv = 0.0;
             if (k2 > 1.0 && A.env_k[e] > 0.0) {
-                const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(p[0], p[0]), __fmul_rn(p[1], p[1])),
-                                                       __fmul_rn(p[2], p[2])));
-                tv = (1.0 - 1.0 / sqrt(k2)) * (double)nrm / A.env_scale[e];
+                const float nrm = igm::sqrtf_rn(__fadd_rn(__fadd_rn(__fmul_rn(p[0], p[0]), __fmul_rn(p[1], p[1])),
+                                                          __fmul_rn(p[2], p[2])));
+                tv = (1.0 - 1.0 / igm::sqrt_rn(k2)) * (double)nrm / A.env_scale[e];
             } else if (k2 < 1.0 && A.env_k[e] < 0.0) {
-                tv = 1.0 - sqrt(k2);
+                tv = 1.0 - igm::sqrt_rn(k2);
             }
             record(he, tv > 0.0 ? tv : 0.0, A.tol);
         }

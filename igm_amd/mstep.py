@@ -118,6 +118,18 @@ def velocity_create(flags, seeds, temperature, ctx=None, device=0):
     return v
 
 
+def act_rows(row, col, dist, prob=None):
+    """actdist.hdf5 datasets -> the igm_actdist_row array the GPU consumes."""
+    from ._lib import row_dtype
+    a = np.zeros(len(row), row_dtype)
+    a['row'] = row
+    a['col'] = col
+    a['dist'] = dist
+    if prob is not None:
+        a['prob'] = prob
+    return a
+
+
 def hic_select(xyz, radii, chrom, act_row, act_col, act_dist, contact_range=2.0, kspring=1.0,
                inter_class=M.CLASS_INTER_HIC, intra_class=M.CLASS_INTRA_HIC, ctx=None, device=0):
     """Per-structure Hi-C bonds (CSR: ptr (S+1), bonds, class)."""
@@ -126,14 +138,11 @@ def hic_select(xyz, radii, chrom, act_row, act_col, act_dist, contact_range=2.0,
     S, N = xyz.shape[0], xyz.shape[1]
     radii = _np(radii, np.float32)
     chrom = _np(chrom, np.int32)
-    row = _np(act_row, np.int32)
-    col = _np(act_col, np.int32)
-    dist = _np(act_dist, np.float32)
+    act = act_rows(act_row, act_col, act_dist)
     ptr = np.zeros(S + 1, np.int64)
     tot = ctypes.c_int64(0)
-    args = [c.h, 0, S, N, xyz.ctypes.data, radii.ctypes.data, chrom.ctypes.data, row.ctypes.data,
-            col.ctypes.data, dist.ctypes.data, len(row), float(contact_range), float(kspring),
-            int(inter_class), int(intra_class), ptr.ctypes.data]
+    args = [c.h, 0, S, N, xyz.ctypes.data, radii.ctypes.data, chrom.ctypes.data, act.ctypes.data,
+            len(act), float(contact_range), float(kspring), int(inter_class), int(intra_class), ptr.ctypes.data]
     rc = c.lib.igm_hic_select(*(args + [None, None, ctypes.byref(tot)]))
     c.check(rc, 'igm_hic_select')
     bonds = np.zeros(max(tot.value, 1), bond_dtype)

@@ -1,0 +1,207 @@
+"""Device-resident A/M iteration (the loop body of bin/igm-run:105-167 for the
+Hi-C hot path) on one GPU per process.
+
+  A-step  ActivationDistanceStep (steps/ActivationDistanceStep.py:111-298)
+  M-step  ModelingStep (steps/ModelingStep.py:105-783) with the LAMMPS kernel
+          replaced by igm_mstep_run
+
+The population never leaves HBM between the steps: the structures of this rank
+are struct-major (S_local, natom, 3) for the M-step; the A-step needs every
+structure of the population, so with several ranks one all_gather (RCCL over
+xGMI) assembles it before the A-step, whose pair list is split into contiguous
+shards; the rows come back in pair order with a second all_gather.  Nothing is
+exchanged during the M-step: structures are independent (ModelingStep.py:164-573
+only touches its own struct_id).
+
+torch is used for device memory, streams and torch.distributed only; every
+computation is a libigmhip.so kernel.
+"""
+import ctypes
+import time
+
+import numpy as np
+
+from . import _lib
+from . import model as M
+from ._lib import IGM_DEVICE_PTRS, bond_dtype, optinfo_dtype, pair_dtype, result_dtype, row_dtype
+
+REC = 104
+
+
+class AMIteration(object):
+    """One GPU's share of a population and the state of the A/M loop."""
+
+    def __init__(self, device, xyz_local, atoms, chrom, copy_ptr, copy_idx, pairs, params, polymer,
+                 seed=6535, contact_range=2.0, kspring=1.0, it_corr=1, tol=0.05, env_scale=(550.0,),
+                 first_sid=0, rank=0, world=1, group=None):
+        import torch
+        self.torch = torch
+        self.dev = torch.device(device)
+        self.rank, self.world, self.group = rank, world, group
+        self.ctx = _lib.context(self.dev.index or 0)
+        T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a if dt is None else a.astype(dt))).to(self.dev)
+        xyz_local = np.ascontiguousarray(xyz_local, np.float32)
+        self.S_local, self.natom = xyz_local.shape[0], xyz_local.shape[1]
+        self.nbead = int(atoms.nbead)
+        self.S_total = self.S_local * world
+        self.xyz = T(xyz_local)                                  # (S_local, natom, 3) M-step layout
+        self.radii = T(atoms.radii)
+        self.flags = T(atoms.flags)
+        self.chrom = T(np.asarray(chrom, np.int32))              # (natom) diploid chrom
+        self.bead_radii = T(atoms.radii[:self.nbead])
+        self.copy_ptr = T(np.asarray(copy_ptr, np.int32))
+        self.copy_idx = T(np.asarray(copy_idx, np.int32))
+        self.hap_chrom = T(np.asarray(chrom, np.int32)[:len(copy_ptr) - 1])
+        # contiguous pair shard of this rank (CSR order is kept across ranks)
+        P = len(pairs)
+        self.pair_lo = P * rank // world
+        self.pair_hi = P * (rank + 1) // world
+        self.npairs_total = P
+        self.pairs = T(np.ascontiguousarray(pairs[self.pair_lo:self.pair_hi], pair_dtype).view(np.uint8))
+        self.npairs = self.pair_hi - self.pair_lo
+        self.per_pair = torch.empty(max(self.npairs, 1) * result_dtype.itemsize, dtype=torch.uint8, device=self.dev)
+        self.params = params
+        self.poly = T(np.ascontiguousarray(polymer, bond_dtype).view(np.uint8))
+        self.npoly = len(polymer)
+        self.poly_cls = T(np.full(len(polymer), M.CLASS_POLYMER, np.int32))
+        self.class_cr = np.array([contact_range, contact_range, contact_range], np.float64)
+        self.env_scale = np.asarray(env_scale, np.float64)
+        self.seed, self.cr, self.kspring, self.it_corr, self.tol = seed, contact_range, kspring, it_corr, tol
+        self.sids = np.arange(first_sid, first_sid + self.S_local)
+        self.step_no = 0
+        self.times = {}
+        # bead-major full population for the A-step
+        self.pop_bm = torch.empty((self.nbead, self.S_total, 3), dtype=torch.float32, device=self.dev)
+        self.gathered = torch.empty((self.S_total, self.natom, 3), dtype=torch.float32, device=self.dev) \
+            if world > 1 else None
+
+    # ------------------------------------------------------------------ helpers
+    def _call(self, fn, *args):
+        c = self.ctx
+        c.set_stream(self.torch.cuda.current_stream(self.dev).cuda_stream)
+        try:
+            c.check(getattr(c.lib, fn)(c.h, *args), fn)
+        finally:
+            c.set_stream(None)
+
+    def _sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    # ------------------------------------------------------------------ A-step
+    def astep(self):
+        torch = self.torch
+        P = _lib.ptr
+        if self.world > 1:
+            torch.distributed.all_gather_into_tensor(self.gathered, self.xyz, group=self.group)
+            src = self.gathered
+        else:
+            src = self.xyz
+        # (S_total, natom, 3) -> (nbead, S_total, 3): the .hss / A-step layout
+        self._call('igm_population_transpose', IGM_DEVICE_PTRS, self.nbead, self.S_total, self.natom, P(src),
+                   P(self.pop_bm), 1)
+        cap = 4 * max(self.npairs, 1)
+        rows = torch.empty(cap * row_dtype.itemsize, dtype=torch.uint8, device=self.dev)
+        n = ctypes.c_int64(0)
+        if self.npairs > 0:
+            self._call('igm_astep_actdist', IGM_DEVICE_PTRS, P(self.pop_bm), self.nbead, self.S_total,
+                       P(self.bead_radii), P(self.copy_ptr), P(self.copy_idx), int(self.copy_ptr.shape[0]) - 1,
+                       P(self.hap_chrom), P(self.pairs), self.npairs, float(self.cr), int(self.it_corr),
+                       P(self.per_pair), P(rows), cap, ctypes.byref(n))
+        nrows = n.value
+        if self.world > 1:
+            counts = torch.tensor([nrows], dtype=torch.int64, device=self.dev)
+            allc = [torch.zeros_like(counts) for _ in range(self.world)]
+            torch.distributed.all_gather(allc, counts, group=self.group)
+            allc = [int(x.item()) for x in allc]
+            mx = max(allc)
+            buf = torch.zeros(max(mx, 1) * row_dtype.itemsize, dtype=torch.uint8, device=self.dev)
+            buf[:nrows * row_dtype.itemsize] = rows[:nrows * row_dtype.itemsize]
+            bufs = [torch.empty_like(buf) for _ in range(self.world)]
+            torch.distributed.all_gather(bufs, buf, group=self.group)
+            rows = torch.cat([b[:c * row_dtype.itemsize] for b, c in zip(bufs, allc)])
+            nrows = sum(allc)
+        self.rows, self.nrows = rows, nrows
+        if self.it_corr == 1 and self.npairs > 0:  # plast of the next iteration (same sigma)
+            self._call('igm_astep_update_plast', IGM_DEVICE_PTRS, P(self.pairs), self.npairs, P(self.per_pair))
+        return nrows
+
+    # ------------------------------------------------------------------ M-step
+    def select(self):
+        """interHiC/intraHiC restraint selection of every local structure from the
+        A-step rows (restraints/inter_hic.py:294-312): per-structure CSR on device."""
+        torch = self.torch
+        P = _lib.ptr
+        S, N = self.S_local, self.natom
+        ptr = torch.empty(S + 1, dtype=torch.int64, device=self.dev)
+        tot = ctypes.c_int64(0)
+        args = [IGM_DEVICE_PTRS, S, N, P(self.xyz), P(self.radii), P(self.chrom), P(self.rows), self.nrows,
+                float(self.cr), float(self.kspring), M.CLASS_INTER_HIC, M.CLASS_INTRA_HIC, P(ptr)]
+        self._call('igm_hic_select', *(args + [None, None, ctypes.byref(tot)]))
+        nb = tot.value
+        bonds = torch.empty(max(nb, 1) * bond_dtype.itemsize, dtype=torch.uint8, device=self.dev)
+        bcls = torch.empty(max(nb, 1), dtype=torch.int32, device=self.dev)
+        self._call('igm_hic_select', *(args + [P(bonds), P(bcls), ctypes.byref(tot)]))
+        self.hic_ptr, self.hic_bonds, self.hic_cls, self.nbonds = ptr, bonds, bcls, nb
+        return ptr, bonds, bcls
+
+    def mstep(self):
+        torch = self.torch
+        P = _lib.ptr
+        S, N = self.S_local, self.natom
+        ptr, bonds, bcls = self.select()
+        seeds = torch.from_numpy(M.lammps_seeds(self.seed, self.sids, self.step_no)).to(self.dev)
+        info = torch.empty(S * optinfo_dtype.itemsize, dtype=torch.uint8, device=self.dev)
+        self._call('igm_mstep_run', IGM_DEVICE_PTRS, ctypes.byref(self.params), S, N, P(self.xyz), P(self.radii),
+                   P(self.flags), P(self.poly), self.npoly, P(ptr), P(bonds), P(seeds), P(info))
+        ncls = len(self.class_cr) + self.params.nenvelopes
+        stats = torch.empty((S, ncls, REC), dtype=torch.int64, device=self.dev)
+        self._call('igm_mstep_violations', IGM_DEVICE_PTRS, ctypes.byref(self.params), S, N, P(self.xyz),
+                   P(self.radii), P(self.flags), P(self.poly), P(self.poly_cls), self.npoly, P(ptr), P(bonds),
+                   P(bcls), len(self.class_cr), self.class_cr.ctypes.data, self.env_scale.ctypes.data,
+                   float(self.tol), P(stats))
+        self.info, self.stats = info, stats
+        self.step_no += 1
+        return stats
+
+    def violation_score(self):
+        """ModelingStep.log_stats: sum n_violations / sum n_imposed (all ranks)."""
+        torch = self.torch
+        v = torch.stack([self.stats[:, :, 102].sum(), self.stats[:, :, 103].sum()]).to(torch.float64)
+        if self.world > 1:
+            torch.distributed.all_reduce(v, group=self.group)
+        nv, ni = float(v[0]), float(v[1])
+        return nv / ni if ni > 0 else 0.0
+
+    def step(self):
+        t0 = time.perf_counter()
+        self.astep()
+        self._sync()
+        t1 = time.perf_counter()
+        self.mstep()
+        self._sync()
+        t2 = time.perf_counter()
+        self.times = {'astep_s': t1 - t0, 'mstep_s': t2 - t1}
+        return self.times
+
+    def info_host(self):
+        return self.info.cpu().numpy().view(optinfo_dtype)
+
+    def anneal_evaluations(self):
+        """Force evaluations of one anneal launch per structure: every 'run n' of the
+        protocol (relax + main run per stage, lammps.py:285-351) is n steps plus the
+        Verlet setup evaluation."""
+        p = self.params
+        n = 0
+        for k in range(p.nstages):
+            if p.relax_steps > 0:
+                n += p.relax_steps + 1
+            n += p.mdsteps[k] + 1
+        return n
+
+    def algorithmic_anneal_bytes(self):
+        """B_eval = 72 N + 4 N + 16 B_bonds bytes per force evaluation
+        per structure (x, v, f f32x3 read+write; radius/flags; bond records), times
+        the evaluations of one anneal launch, summed over this rank's structures."""
+        ptr = self.hic_ptr.cpu().numpy()
+        bonds_per = np.diff(ptr) + self.npoly
+        return float(np.sum(76.0 * self.natom + 16.0 * bonds_per) * self.anneal_evaluations())

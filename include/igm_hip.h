@@ -94,6 +94,12 @@ int igm_astep_actdist(igm_ctx* ctx, uint32_t flags,
                       igm_actdist_row* rows, int64_t row_capacity,       /* CSR pair order   */
                       int64_t* nrows_out);                               /* host pointer     */
 
+/* Next-iteration plast (ActivationDistanceStep.setup:144-160 applied to the rows
+ * this A-step emitted): pairs[q].plast = float32('%.4f' % p_q) if the pair emitted
+ * rows, else 0.  Valid when the same pair list is used again (same sigma). */
+int igm_astep_update_plast(igm_ctx* ctx, uint32_t flags, igm_pair* pairs, int64_t npairs,
+                           const igm_pair_result* per_pair);
+
 /* ---- M-step ---------------------------------------------------------------
  * Batched replacement of lammps.optimize (lammps.py:361-492): the protocol of
  * create_lammps_script (lammps.py:149-358) -- per stage: fix adapt of the soft
@@ -199,7 +205,7 @@ int igm_velocity_create(igm_ctx* ctx, uint32_t flags, int32_t nseed, int32_t nat
  * interHiC/intraHiC._apply (restraints/inter_hic.py:294-312, intra_hic.py) for
  * every actdist row and every structure: a bond (i, j) is imposed when
  * ||x_i - x_j|| <= dist (f32, no FMA) and the chromosome test holds.
- *   xyz (nstruct, natom, 3) struct-major; act rows (n_act) from actdist.hdf5;
+ *   xyz (nstruct, natom, 3) struct-major; act rows (n_act): igm_astep_actdist output;
  *   chrom (natom); output per-structure CSR of bonds, inter rows first then
  *   intra rows (the reference order), r0 = cr*(r_i + r_j), k; out_class (may be
  *   NULL) receives inter_class / intra_class for each bond (violation classes).
@@ -208,10 +214,17 @@ int igm_velocity_create(igm_ctx* ctx, uint32_t flags, int32_t nseed, int32_t nat
 int igm_hic_select(igm_ctx* ctx, uint32_t flags,
                    int32_t nstruct, int32_t natom, const float* xyz,
                    const float* radii, const int32_t* chrom,
-                   const int32_t* act_row, const int32_t* act_col, const float* act_dist,
+                   const igm_actdist_row* act, /* the A-step rows (actdist.hdf5 row/col/dist/prob) */
                    int64_t n_act, double contact_range, double kspring,
                    int32_t inter_class, int32_t intra_class,
                    int64_t* out_ptr, igm_bond* out_bonds, int32_t* out_class, int64_t* ntotal);
+
+/* Population layout change between the .hss / A-step layout (bead-major
+ * (nbead, nstruct, 3), core/step.py:373) and the M-step layout (struct-major
+ * (nstruct, natom, 3), natom >= nbead; extra atoms left untouched).
+ * direction 0: bead-major -> struct-major; 1: struct-major -> bead-major. */
+int igm_population_transpose(igm_ctx* ctx, uint32_t flags, int32_t nbead, int32_t nstruct, int32_t natom,
+                             const float* src, float* dst, int32_t direction);
 
 /* ---- M-step violation scoring (ModelingStep.py:511-557,859-869) ------------
  * For each structure and each restraint class c -- bond classes 0..nclass_bonds-1

@@ -7,17 +7,7 @@ import numpy as np
 
 from conftest import GOLDEN
 
-DEMO_PROTOCOL = {
-    # demo/config_file.json optimizer_options (the reference demo), copied as data
-    "mdsteps": 45000, "timestep": 0.25, "tstart": 500.0, "tstop": 0.01,
-    "custom_annealing_protocol": {
-        "num_steps": 4, "mdsteps": [5000, 15000, 15000, 10000],
-        "tstarts": [5000.0, 500.0, 50.0, 1.0], "tstops": [500.0, 50.0, 1.0, 0.0],
-        "evfactors": [0.5, 1.0, 1.0, 1.0], "envelope_factors": [1.2, 1.0, 1.0, 1.0],
-        "relax": {"mdsteps": 500, "temperature": 1.0, "max_velocity": 10.0}},
-    "damp": 50.0, "max_velocity": 1000.0, "etol": 0.0001, "ftol": 1e-06,
-    "max_cg_iter": 500, "max_cg_eval": 500, "thermo": 1000, "write": -1,
-}
+from igm_amd.synthetic import DEMO_PROTOCOL  # noqa: E402  (demo/config_file.json optimizer_options)
 
 
 def load():

@@ -5,6 +5,8 @@ import pytest
 
 from conftest import make_pairs
 
+import oracle
+
 pytestmark = pytest.mark.gpu
 
 SIGMAS = [1.0, 0.2, 0.05, 0.02]
@@ -138,6 +140,16 @@ def test_gpu_get_actdist_signature(astep, demo_pop):
         def get_bead_crd(self, k):
             return self.p['coordinates'][k]
 
-    res = astep.get_actdist(0, 5, 0.3, 0.0, Hss(demo_pop), 1, contactRange=2.0)
-    assert len(res) == 2 and res[0][0] == 0 and res[0][1] == 5 and res[1][0] == 1558
-    assert astep.get_actdist(3, 3, 0.3, 0.0, Hss(demo_pop), 1) == []
+    p = demo_pop
+    for (i, j, pw, it_corr) in [(0, 5, 0.3, 0), (0, 5, 0.3, 1), (2, 40, 0.05, 0), (0, 1500, 0.02, 0)]:
+        res = astep.get_actdist(i, j, pw, 0.0, Hss(p), it_corr, contactRange=2.0)
+        _, ores = oracle.actdist(p['coordinates'], p['radii'], p['copy_ptr'], p['copy_idx'], p['chrom'],
+                                 make_pairs([i], [j], [pw], [0.0]), 2.0, it_corr)
+        if ores['nrows'][0] == 0:
+            assert res == []
+            continue
+        ci = [list(p['copy_idx'][p['copy_ptr'][h]:p['copy_ptr'][h + 1]]) for h in (i, j)]
+        combos = list(zip(*ci)) if p['chrom'][i] == p['chrom'][j] else [(a, b) for a in ci[0] for b in ci[1]]
+        assert [(r[0], r[1]) for r in res] == combos
+        assert all(r[2] == ores['ad'][0] and r[3] == ores['p'][0] for r in res)
+    assert astep.get_actdist(3, 3, 0.3, 0.0, Hss(p), 1) == []
