@@ -21,7 +21,11 @@
 namespace {
 
 constexpr int kWavesPerBlock = 4;
-constexpr int kBuckets = 9;  // VPL 1..64 (7 buckets) + unsupported + no-combination
+// buckets: 0..6 one wave per pair with VPL 1..64 keys per lane; 7 unsupported;
+// 8 no combination; 9..12 one 1024-thread workgroup per pair with VPL 8..64
+// keys per thread (populations too large for one wave's registers).
+constexpr int kBuckets = 13;
+constexpr int kBlockThreads = 1024;
 
 __device__ __forceinline__ int pair_ncomb(const int* copy_ptr, const int* chrom, int i, int j, int nhap, int* na,
                                           int* nb, bool* intra) {
@@ -45,13 +49,20 @@ __global__ void classify_kernel(const igm_pair* __restrict__ pairs, int64_t npai
     if (n <= 0) {
         b = 8;
     } else {
-        int need = n * ((S + 63) / 64);
+        const int64_t need = (int64_t)n * ((S + 63) / 64);
+        const int64_t keys = (int64_t)n * S;
         b = 7;
         for (int k = 0, v = 1; k < 7; ++k, v <<= 1)
             if (need <= v) {
                 b = k;
                 break;
             }
+        if (b == 7)
+            for (int k = 0, v = 8; k < 4; ++k, v <<= 1)
+                if (keys <= (int64_t)kBlockThreads * v) {
+                    b = 9 + k;
+                    break;
+                }
     }
     int slot = atomicAdd(&counts[b], 1);
     lists[(int64_t)b * npairs + slot] = (int)q;
@@ -85,6 +96,47 @@ __device__ __forceinline__ double round_dec4(double x) {
 __device__ __forceinline__ double clean_prob(double pij, double pexist) {
     double pc = (pexist < 1.0) ? (pij - pexist) / (1.0 - pexist) : pij;
     return pc > 0.0 ? pc : 0.0;  // Python max(0, pc): 0 when pc <= 0 (or NaN)
+}
+
+// rcutsq = (cr*(ri+rj))^2: ri+rj in f32, the rest in f64 (NumPy 1.x scalar
+// promotion, py:393-396); returns the largest float key f with (double)f <= rcutsq,
+// so that  d2 <= f  <=>  (double)d2 <= rcutsq.
+__device__ __forceinline__ uint32_t cut_key(const float* radii, const int* copy_idx, int a0, int b0, double cr) {
+    const float rsum = __fadd_rn(radii[copy_idx[a0]], radii[copy_idx[b0]]);
+    const double rc = cr * (double)rsum;
+    const double rcutsq = rc * rc;
+    float fthr = (float)rcutsq;
+    if ((double)fthr > rcutsq) fthr = nextafterf(fthr, 0.0f);
+    return __float_as_uint(fthr);
+}
+
+// pnow, the corrected probability and the order index o (py:445-476); returns o,
+// or -1 when the pair emits nothing (r filled completely then)
+__device__ __forceinline__ int64_t pair_order(int cnt, int n, int S, const igm_pair& pr, int it_corr,
+                                              igm_pair_result* r) {
+    const int64_t nS = (int64_t)n * S;
+    const double pnow = (double)cnt / (double)nS;  // py:445
+    double p;
+    if (it_corr == 1) {  // py:452-459
+        const double tcorr = clean_prob(pnow, pr.plast);
+        p = clean_prob(pr.pwish, tcorr);
+    } else {
+        p = pr.pwish;
+    }
+    r->p = p;
+    r->pnow = pnow;
+    if (!(p > 0.0)) {
+        r->ad = __longlong_as_double(0x7ff8000000000000LL);
+        r->o = -1;
+        r->nrows = 0;
+        return -1;
+    }
+    // o = min(nS - 1, int(round(n * p * S)))   (py:469-470, banker's rounding)
+    const double ox = rint((double)n * p * (double)S);
+    const int64_t o = (ox >= (double)(nS - 1)) ? nS - 1 : (int64_t)ox;
+    r->o = (int)o;
+    r->nrows = n;  // py:476-483: zip(ii,jj) or the ii x jj product
+    return o;
 }
 
 template <int VPL>
@@ -134,39 +186,13 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock)
         }
     }
 
-    // ---- rcutsq = (cr*(ri+rj))^2: ri+rj in f32, the rest in f64 (NumPy 1.x scalar promotion, py:393-396)
-    const float rsum = __fadd_rn(radii[copy_idx[a0]], radii[copy_idx[b0]]);
-    const double rc = cr * (double)rsum;
-    const double rcutsq = rc * rc;
-    // largest float f with (double)f <= rcutsq: d2 <= f  <=>  (double)d2 <= rcutsq
-    float fthr = (float)rcutsq;
-    if ((double)fthr > rcutsq) fthr = nextafterf(fthr, 0.0f);
-    const uint32_t thr = __float_as_uint(fthr);
-
+    const uint32_t thr = cut_key(radii, copy_idx, a0, b0, cr);
     int cnt = 0;
 #pragma unroll
     for (int t = 0; t < VPL; ++t) cnt += __popcll(__ballot(key[t] <= thr));
-
-    const int64_t nS = (int64_t)n * S;
-    const double pnow = (double)cnt / (double)nS;  // py:445
-    double p;
-    if (it_corr == 1) {  // py:452-459
-        const double tcorr = clean_prob(pnow, pr.plast);
-        p = clean_prob(pr.pwish, tcorr);
-    } else {
-        p = pr.pwish;
-    }
     igm_pair_result r;
-    r.p = p;
-    r.pnow = pnow;
-    if (!(p > 0.0)) {
-        r.ad = __longlong_as_double(0x7ff8000000000000LL);
-        r.o = -1;
-        r.nrows = 0;
-    } else {
-        // o = min(nS - 1, int(round(n * p * S)))   (py:469-470, banker's rounding)
-        const double ox = rint((double)n * p * (double)S);
-        int64_t o = (ox >= (double)(nS - 1)) ? nS - 1 : (int64_t)ox;
+    const int64_t o = pair_order(cnt, n, S, pr, it_corr, &r);
+    if (o >= 0) {
         // o-th smallest key by bisection on the bit pattern
         uint32_t lo = 0u, hi = 0xFFFFFFFEu;
         const int target = (int)o + 1;
@@ -181,10 +207,85 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock)
                 lo = mid + 1u;
         }
         r.ad = sqrt_rn((double)__uint_as_float(lo));  // py:473
-        r.o = (int)o;
-        r.nrows = n;  // py:476-483: zip(ii,jj) or the ii x jj product
     }
     if (lane == 0) res[q] = r;
+}
+
+// Same contract for populations whose n*S keys exceed one wave's registers: a
+// 1024-thread workgroup per pair, key e = t + k*1024 over the flattened
+// (combination, structure) range, block-wide counts through LDS.
+template <int VPL>
+__global__ void __launch_bounds__(kBlockThreads)
+    actdist_block_kernel(const float* __restrict__ xyz, int S, const float* __restrict__ radii,
+                         const int* __restrict__ copy_ptr, const int* __restrict__ copy_idx,
+                         const int* __restrict__ chrom, int nhap, const igm_pair* __restrict__ pairs,
+                         const int* __restrict__ list, int nlist, double cr, int it_corr,
+                         igm_pair_result* __restrict__ res) {
+    __shared__ int part[2][kBlockThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int q = list[blockIdx.x];
+    const igm_pair pr = pairs[q];
+    int na = 0, nb = 0;
+    bool intra = false;
+    const int n = pair_ncomb(copy_ptr, chrom, pr.i, pr.j, nhap, &na, &nb, &intra);
+    const int a0 = copy_ptr[pr.i], b0 = copy_ptr[pr.j];
+    const int nk = n * S;
+    uint32_t key[VPL];
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+        key[k] = 0xFFFFFFFFu;
+        const int e = k * kBlockThreads + t;
+        if (e < nk) {
+            const int c = e / S, s = e - c * S;
+            int ka, m;
+            if (intra) {
+                ka = copy_idx[a0 + c];
+                m = copy_idx[b0 + c];
+            } else {
+                ka = copy_idx[a0 + c / nb];
+                m = copy_idx[b0 + c % nb];
+            }
+            const float* xk = xyz + ((size_t)ka * S + s) * 3;
+            const float* xm = xyz + ((size_t)m * S + s) * 3;
+            const float dx = __fsub_rn(xk[0], xm[0]);
+            const float dy = __fsub_rn(xk[1], xm[1]);
+            const float dz = __fsub_rn(xk[2], xm[2]);
+            key[k] = __float_as_uint(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+        }
+    }
+    int it = 0;
+    // block-wide count of keys <= v (alternating LDS buffers: one barrier per count)
+    auto count_le = [&](uint32_t v) {
+        int cm = 0;
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) cm += key[k] <= v;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) cm += __shfl_xor(cm, off);
+        int* buf = part[it & 1];
+        ++it;
+        if (lane == 0) buf[w] = cm;
+        __syncthreads();
+        int tot = 0;
+#pragma unroll
+        for (int i = 0; i < kBlockThreads / 64; ++i) tot += buf[i];
+        return tot;
+    };
+    const int cnt = count_le(cut_key(radii, copy_idx, a0, b0, cr));
+    igm_pair_result r;
+    const int64_t o = pair_order(cnt, n, S, pr, it_corr, &r);
+    if (o >= 0) {
+        uint32_t lo = 0u, hi = 0xFFFFFFFEu;
+        const int target = (int)o + 1;
+        while (lo < hi) {
+            const uint32_t mid = lo + ((hi - lo) >> 1);
+            if (count_le(mid) >= target)
+                hi = mid;
+            else
+                lo = mid + 1u;
+        }
+        r.ad = sqrt_rn((double)__uint_as_float(lo));  // py:473
+    }
+    if (t == 0) res[q] = r;
 }
 
 __global__ void nrows_kernel(const igm_pair_result* __restrict__ res, int64_t npairs, int64_t* __restrict__ nr) {
@@ -243,6 +344,17 @@ int launch_bucket(igm_ctx* c, const float* xyz, int S, const float* radii, const
     dim3 grid((unsigned)igm::ceil_div(nlist, kWavesPerBlock));
     hipLaunchKernelGGL(actdist_kernel<VPL>, grid, dim3(64 * kWavesPerBlock), 0, c->stream, xyz, S, radii, cptr, cidx,
                        chrom, nhap, pairs, list, nlist, cr, it_corr, res);
+    IGM_HIP_CHECK(c, hipGetLastError());
+    return IGM_OK;
+}
+
+template <int VPL>
+int launch_block_bucket(igm_ctx* c, const float* xyz, int S, const float* radii, const int* cptr, const int* cidx,
+                        const int* chrom, int nhap, const igm_pair* pairs, const int* list, int nlist, double cr,
+                        int it_corr, igm_pair_result* res) {
+    if (nlist <= 0) return IGM_OK;
+    hipLaunchKernelGGL(actdist_block_kernel<VPL>, dim3((unsigned)nlist), dim3(kBlockThreads), 0, c->stream, xyz, S,
+                       radii, cptr, cidx, chrom, nhap, pairs, list, nlist, cr, it_corr, res);
     IGM_HIP_CHECK(c, hipGetLastError());
     return IGM_OK;
 }
@@ -309,9 +421,9 @@ extern "C" int igm_astep_actdist(igm_ctx* c, uint32_t flags, const float* xyz, i
         IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
         if (h_counts[7] > 0)
             return fail(c, IGM_E_UNSUPPORTED,
-                        "igm_astep_actdist: %d pairs need n_combinations*ceil(S/64) > 64 (S=%d); "
-                        "population too large for the register-resident selection kernel",
-                        h_counts[7], nstruct);
+                        "igm_astep_actdist: %d pairs need n_combinations*S > %d keys (S=%d); "
+                        "population too large for the register-resident selection kernels",
+                        h_counts[7], 64 * kBlockThreads, nstruct);
         const int* L = d_lists;
         Timed tm(c, "actdist");  // the selection kernels only (inputs resident)
         IGM_TRY(launch_bucket<1>(c, d_xyz, nstruct, d_radii, d_cptr, d_cidx, d_chrom, nhap, d_pairs, L + 0 * npairs,
@@ -328,6 +440,14 @@ extern "C" int igm_astep_actdist(igm_ctx* c, uint32_t flags, const float* xyz, i
                                   h_counts[5], contact_range, it_corr, d_res));
         IGM_TRY(launch_bucket<64>(c, d_xyz, nstruct, d_radii, d_cptr, d_cidx, d_chrom, nhap, d_pairs, L + 6 * npairs,
                                   h_counts[6], contact_range, it_corr, d_res));
+        IGM_TRY(launch_block_bucket<8>(c, d_xyz, nstruct, d_radii, d_cptr, d_cidx, d_chrom, nhap, d_pairs,
+                                       L + 9 * npairs, h_counts[9], contact_range, it_corr, d_res));
+        IGM_TRY(launch_block_bucket<16>(c, d_xyz, nstruct, d_radii, d_cptr, d_cidx, d_chrom, nhap, d_pairs,
+                                        L + 10 * npairs, h_counts[10], contact_range, it_corr, d_res));
+        IGM_TRY(launch_block_bucket<32>(c, d_xyz, nstruct, d_radii, d_cptr, d_cidx, d_chrom, nhap, d_pairs,
+                                        L + 11 * npairs, h_counts[11], contact_range, it_corr, d_res));
+        IGM_TRY(launch_block_bucket<64>(c, d_xyz, nstruct, d_radii, d_cptr, d_cidx, d_chrom, nhap, d_pairs,
+                                        L + 12 * npairs, h_counts[12], contact_range, it_corr, d_res));
         if (h_counts[8] > 0) {
             hipLaunchKernelGGL(mark_unprocessed, dim3((unsigned)ceil_div(h_counts[8], 256)), dim3(256), 0, c->stream,
                                d_res, L + 8 * npairs, h_counts[8]);

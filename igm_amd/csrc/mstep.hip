@@ -30,6 +30,10 @@ namespace igm {
 namespace ms {
 
 constexpr uint32_t kLowerBit = 0x80000000u;
+// nnb value of an atom with more list candidates than the capacity: its pair
+// forces are taken by walking the 27 cells of the build-time grid, which
+// visits a superset of its list in the same order (so no overflow error).
+constexpr int kNnbWalk = 0xFFFF;
 constexpr int kMaxTypes = 2048;  // distinct radii (LAMMPS atom types); the pair table is kMaxTypes^2
 
 struct Bonds {
@@ -204,6 +208,11 @@ __device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, i
         }
     }
     const int ncell = nb[0] * nb[1] * nb[2];
+    if (t == 0) {  // for the cell walk of atoms past the list capacity (before the barrier below)
+        sm.misc[4] = nb[0];
+        sm.misc[5] = nb[1];
+        sm.misc[6] = nb[2];
+    }
     for (int c = t; c <= ncell; c += NT) sm.cell[c] = 0;
     __syncthreads();
     for (int b = 0; b < BPT; ++b) {
@@ -244,6 +253,7 @@ __device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, i
         }
     }
     __syncthreads();
+    (void)error;
     const T cut2 = cut_list * cut_list;
     for (int b = 0; b < BPT; ++b) {
         const int a = b * NT + t;
@@ -275,10 +285,7 @@ __device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, i
                     }
                 }
             }
-            if (cnt > kcap) {
-                atomicOr(error, 1);
-                cnt = kcap;
-            }
+            if (cnt > kcap) cnt = kNnbWalk;  // the force routine walks the cells instead
         }
         sm.nnb[a] = (uint16_t)cnt;
     }
@@ -287,37 +294,86 @@ __device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, i
 // ------------------------------------------------------------- forces
 // force (and energy if EN) on atom a; position p0 (w: f32 radius / f64 atom type, <0: no pair)
 template <typename T, bool EN>
+__device__ __forceinline__ void pair_one(int j, T xi, T yi, T zi, T ri, const vec4_t<T>* pos, const DevParams& P,
+                                         T evf, T& fx, T& fy, T& fz, double& ep) {
+    const vec4_t<T> p = pos[j];
+    const T dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
+    double e = 0.0;
+    T fp;
+    if constexpr (std::is_same<T, float>::value) {
+        fp = soft_pair<T, EN>(dx * dx + dy * dy + dz * dz, ri + (T)p.w, evf, e);
+    } else {
+        const double2 pc = P.pair_tab[(int)ri * P.ntype + (int)p.w];
+        fp = soft_pair_typed(dx * dx + dy * dy + dz * dz, pc.x, pc.y, evf, e);
+    }
+    fx += fp * dx;
+    fy += fp * dy;
+    fz += fp * dz;
+    if (EN) ep += 0.5 * e;
+}
+
+// the build-time cell grid (LDS), used for atoms past the list capacity
+struct CellGrid {
+    const int* cell;
+    const uint16_t* sorted;
+    const uint16_t* cellid;
+    const int* dims;  // sm.misc + 4
+};
+
+template <typename T, bool EN>
+__device__ __noinline__ void pair_walk(int a, T xi, T yi, T zi, T ri, const vec4_t<T>* pos, CellGrid g,
+                                       const DevParams& P, T evf, T* f, double* ep) {
+    const int nx = g.dims[0], ny = g.dims[1], nz = g.dims[2];
+    const int c = g.cellid[a];
+    const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+    T fx = f[0], fy = f[1], fz = f[2];
+    double e = *ep;
+    for (int dz = -1; dz <= 1; ++dz) {
+        const int z0 = cz + dz;
+        if (z0 < 0 || z0 >= nz) continue;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int y0 = cy + dy;
+            if (y0 < 0 || y0 >= ny) continue;
+            const int row = (z0 * ny + y0) * nx;
+            const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
+            const int beg = g.cell[row + xlo], end = g.cell[row + xhi + 1];
+            for (int q = beg; q < end; ++q) {
+                const int j = g.sorted[q];
+                if (j != a) pair_one<T, EN>(j, xi, yi, zi, ri, pos, P, evf, fx, fy, fz, e);
+            }
+        }
+    }
+    f[0] = fx;
+    f[1] = fy;
+    f[2] = fz;
+    *ep = e;
+}
+
+template <typename T, bool EN>
 __device__ __forceinline__ void atom_force(int a, const vec4_t<T>& p0, uint32_t fl, const vec4_t<T>* pos,
                                            const uint16_t* nl, int nn, const int4* al, int nd, const DevParams& P,
-                                           T evf, T envf, T& fx, T& fy, T& fz, double& ep, double& eb,
-                                           double (&ee)[IGM_MAX_ENVELOPES]) {
+                                           CellGrid grid, T evf, T envf, T& fx, T& fy, T& fz, double& ep,
+                                           double& eb, double (&ee)[IGM_MAX_ENVELOPES]) {
     fx = fy = fz = T(0);
     const T xi = p0.x, yi = p0.y, zi = p0.z;
     const T ri = (T)p0.w;
     constexpr int U = 8;  // neighbour indices fetched per batch: one memory wait per U pairs
-    if (ri >= T(0)) {
+    if (ri >= T(0) && nn == kNnbWalk) {
+        T f3[3] = {T(0), T(0), T(0)};
+        double e = 0.0;
+        pair_walk<T, EN>(a, xi, yi, zi, ri, pos, grid, P, evf, f3, &e);
+        fx = f3[0];
+        fy = f3[1];
+        fz = f3[2];
+        if (EN) ep += e;
+    } else if (ri >= T(0)) {
         for (int k0 = 0; k0 < nn; k0 += U) {
             int jv[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) jv[u] = (k0 + u < nn) ? (int)nl[(size_t)(k0 + u) * 64] : -1;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (jv[u] < 0) continue;
-                const vec4_t<T> p = pos[jv[u]];
-                const T dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
-                double e = 0.0;
-                T fp;
-                if constexpr (std::is_same<T, float>::value) {
-                    fp = soft_pair<T, EN>(dx * dx + dy * dy + dz * dz, ri + (T)p.w, evf, e);
-                } else {
-                    const double2 pc = P.pair_tab[(int)ri * P.ntype + (int)p.w];
-                    fp = soft_pair_typed(dx * dx + dy * dy + dz * dz, pc.x, pc.y, evf, e);
-                }
-                fx += fp * dx;
-                fy += fp * dy;
-                fz += fp * dz;
-                if (EN) ep += 0.5 * e;
-            }
+            for (int u = 0; u < U; ++u)
+                if (jv[u] >= 0) pair_one<T, EN>(jv[u], xi, yi, zi, ri, pos, P, evf, fx, fy, fz, ep);
         }
     }
     constexpr int UB = 4;  // bond entries (16 B) per batch
@@ -489,7 +545,9 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                     float fx, fy, fz;
                     atom_force<float, false>(a, sm.pos[a], A.cm.aflags[a], sm.pos,
                                              nbr + (size_t)(a >> 6) * A.cm.kcap * 64 + lane, sm.nnb[a],
-                                             adj + soff[a >> 6] + lane, deg[a], A.P, evf, envf, fx, fy, fz, ep, eb,
+                                             adj + soff[a >> 6] + lane, deg[a], A.P,
+                                             CellGrid{sm.cell, sm.sorted, sm.cellid, sm.misc + 4}, evf, envf, fx,
+                                             fy, fz, ep, eb,
                                              ee);
                     sm.frc[a] = make_float4(fx, fy, fz, 0.f);
                 }
@@ -715,7 +773,9 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
                 double fx, fy, fz;
                 atom_force<double, true>(a, sm.pos[a], A.cm.aflags[a], sm.pos,
                                          nbr + (size_t)(a >> 6) * A.cm.kcap * 64 + lane, sm.nnb[a],
-                                         adj + soff[a >> 6] + lane, deg[a], A.P, A.evf, A.envf, fx, fy, fz, vv[0],
+                                         adj + soff[a >> 6] + lane, deg[a], A.P,
+                                         CellGrid{sm.cell, sm.sorted, sm.cellid, sm.misc + 4}, A.evf, A.envf, fx,
+                                         fy, fz, vv[0],
                                          vv[1], e_e);
                 for (int e = 0; e < IGM_MAX_ENVELOPES; ++e) vv[2 + e] += e_e[e];
                 F[a] = fx;
@@ -1095,7 +1155,8 @@ int make_devparams(igm_ctx* c, const igm_mstep_params* prm, int natom, const flo
     }
     P->skin = prm->skin > 0 ? (float)prm->skin : rmax;  // LAMMPS 'neighbor maxrad bin'
     P->cut_list = 2.0f * rmax + P->skin;
-    P->kcap = prm->neigh_capacity > 0 ? prm->neigh_capacity : 96;
+    P->kcap = prm->neigh_capacity > 0 ? prm->neigh_capacity : 128;
+    if (P->kcap >= kNnbWalk) return fail(c, IGM_E_INVALID, "neigh_capacity must be < %d", kNnbWalk);
     P->natom = natom;
     P->nslice = (natom + 63) / 64;
     // atom types: one per distinct f32 radius, in order of first appearance

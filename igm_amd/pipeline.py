@@ -28,6 +28,53 @@ from ._lib import IGM_DEVICE_PTRS, bond_dtype, optinfo_dtype, pair_dtype, result
 REC = 104
 
 
+# ------------------------------------------------------------------ sharding
+def shard(n, rank, world):
+    """Contiguous block [lo, hi) of n units owned by `rank`: structures
+    for the M-step, CSR-ordered pairs for the A-step."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def gather_population(xyz_local, group=None):
+    """Every rank's (S_local, natom, 3) block -> the (S_total, natom, 3) population
+    in rank order (one all-gather; RCCL over xGMI on the GPUs)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(xyz_local) for _ in range(world)]
+    dist.all_gather(parts, xyz_local.contiguous(), group=group)
+    return torch.cat(parts, 0)
+
+
+def gather_rows(rows_u8, nrows, itemsize, group=None):
+    """Concatenate the ranks' A-step rows in rank order, i.e. in CSR pair order
+    (task() appends pair after pair, ActivationDistanceStep.py:228-230): the result
+    is byte-identical to one rank processing every pair."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = rows_u8.device
+    counts = torch.tensor([int(nrows)], dtype=torch.int64, device=dev)
+    allc = [torch.zeros_like(counts) for _ in range(world)]
+    dist.all_gather(allc, counts, group=group)
+    allc = [int(x.item()) for x in allc]
+    mx = max(max(allc), 1)
+    buf = torch.zeros(mx * itemsize, dtype=torch.uint8, device=dev)
+    buf[:nrows * itemsize] = rows_u8[:nrows * itemsize]
+    bufs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf, group=group)
+    return torch.cat([b[:c * itemsize] for b, c in zip(bufs, allc)]), sum(allc)
+
+
+def reduce_sum_f64(values, device, group=None):
+    """Sum a few host numbers over the ranks (violation counts of log_stats)."""
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor(values, dtype=torch.float64, device=device)
+    dist.all_reduce(v, group=group)
+    return v.cpu().numpy()
+
+
 class AMIteration(object):
     """One GPU's share of a population and the state of the A/M loop."""
 
@@ -54,8 +101,7 @@ class AMIteration(object):
         self.hap_chrom = T(np.asarray(chrom, np.int32)[:len(copy_ptr) - 1])
         # contiguous pair shard of this rank (CSR order is kept across ranks)
         P = len(pairs)
-        self.pair_lo = P * rank // world
-        self.pair_hi = P * (rank + 1) // world
+        self.pair_lo, self.pair_hi = shard(P, rank, world)
         self.npairs_total = P
         self.pairs = T(np.ascontiguousarray(pairs[self.pair_lo:self.pair_hi], pair_dtype).view(np.uint8))
         self.npairs = self.pair_hi - self.pair_lo
@@ -72,8 +118,6 @@ class AMIteration(object):
         self.times = {}
         # bead-major full population for the A-step
         self.pop_bm = torch.empty((self.nbead, self.S_total, 3), dtype=torch.float32, device=self.dev)
-        self.gathered = torch.empty((self.S_total, self.natom, 3), dtype=torch.float32, device=self.dev) \
-            if world > 1 else None
 
     # ------------------------------------------------------------------ helpers
     def _call(self, fn, *args):
@@ -92,8 +136,7 @@ class AMIteration(object):
         torch = self.torch
         P = _lib.ptr
         if self.world > 1:
-            torch.distributed.all_gather_into_tensor(self.gathered, self.xyz, group=self.group)
-            src = self.gathered
+            src = gather_population(self.xyz, self.group)
         else:
             src = self.xyz
         # (S_total, natom, 3) -> (nbead, S_total, 3): the .hss / A-step layout
@@ -109,17 +152,7 @@ class AMIteration(object):
                        P(self.per_pair), P(rows), cap, ctypes.byref(n))
         nrows = n.value
         if self.world > 1:
-            counts = torch.tensor([nrows], dtype=torch.int64, device=self.dev)
-            allc = [torch.zeros_like(counts) for _ in range(self.world)]
-            torch.distributed.all_gather(allc, counts, group=self.group)
-            allc = [int(x.item()) for x in allc]
-            mx = max(allc)
-            buf = torch.zeros(max(mx, 1) * row_dtype.itemsize, dtype=torch.uint8, device=self.dev)
-            buf[:nrows * row_dtype.itemsize] = rows[:nrows * row_dtype.itemsize]
-            bufs = [torch.empty_like(buf) for _ in range(self.world)]
-            torch.distributed.all_gather(bufs, buf, group=self.group)
-            rows = torch.cat([b[:c * row_dtype.itemsize] for b, c in zip(bufs, allc)])
-            nrows = sum(allc)
+            rows, nrows = gather_rows(rows, nrows, row_dtype.itemsize, self.group)
         self.rows, self.nrows = rows, nrows
         if self.it_corr == 1 and self.npairs > 0:  # plast of the next iteration (same sigma)
             self._call('igm_astep_update_plast', IGM_DEVICE_PTRS, P(self.pairs), self.npairs, P(self.per_pair))
@@ -165,11 +198,9 @@ class AMIteration(object):
 
     def violation_score(self):
         """ModelingStep.log_stats: sum n_violations / sum n_imposed (all ranks)."""
-        torch = self.torch
-        v = torch.stack([self.stats[:, :, 102].sum(), self.stats[:, :, 103].sum()]).to(torch.float64)
+        nv, ni = float(self.stats[:, :, 102].sum()), float(self.stats[:, :, 103].sum())
         if self.world > 1:
-            torch.distributed.all_reduce(v, group=self.group)
-        nv, ni = float(v[0]), float(v[1])
+            nv, ni = reduce_sum_f64([nv, ni], self.dev, self.group)
         return nv / ni if ni > 0 else 0.0
 
     def step(self):

@@ -95,6 +95,34 @@ def test_gpu_vs_oracle_population_1000(astep, demo_pop, demo_pairs):
         assert rows.tobytes() == orows.tobytes()
 
 
+@pytest.mark.parametrize('reps', [11, 80])
+def test_gpu_vs_oracle_large_population(astep, demo_pop, demo_pairs, reps):
+    """Populations past one wave's registers (S = 1100: inter pairs need the
+    workgroup kernel; S = 8000: the 8-GPU weak-scaling population, every pair
+    on the workgroup kernel): rows bit-identical to the oracle."""
+    import oracle
+    rng = np.random.default_rng(12 + reps)
+    base = demo_pop['coordinates']
+    xyz = np.concatenate([base + rng.normal(0, 50.0, base.shape).astype(np.float32) for _ in range(reps)], axis=1)
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    keep = np.where(demo_pairs['p'] >= 0.02)[0]
+    sub = keep[rng.choice(len(keep), 400, replace=False)]
+    sub.sort()
+    pairs = make_pairs(demo_pairs['i'][sub], demo_pairs['j'][sub], demo_pairs['p'][sub].astype(np.float64),
+                       rng.uniform(0, 0.5, len(sub)))
+    for it_corr in (0, 1):
+        rows, res = astep.compute_actdist(xyz, demo_pop['radii'], demo_pop['copy_ptr'], demo_pop['copy_idx'],
+                                          demo_pop['chrom'], pairs, 2.0, it_corr, return_per_pair=True)
+        orows, ores = oracle.actdist(xyz, demo_pop['radii'], demo_pop['copy_ptr'], demo_pop['copy_idx'],
+                                     demo_pop['chrom'], pairs, 2.0, it_corr, nthreads=16)
+        assert np.array_equal(res['nrows'], ores['nrows'])
+        assert np.array_equal(res['o'], ores['o'])
+        assert np.array_equal(res['pnow'], ores['pnow'])
+        has = res['nrows'] > 0
+        assert np.array_equal(res['ad'][has], ores['ad'][has])
+        assert rows.tobytes() == orows.tobytes()
+
+
 def test_gpu_device_pointer_path(astep, demo_pop, demo_pairs, g1):
     """Inputs already resident in HBM (torch tensors): same rows as the host path."""
     import torch

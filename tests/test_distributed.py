@@ -1,0 +1,80 @@
+"""The N>1 data path of igm_amd.pipeline on CPU (gloo, world_size 2): structure
+shards -> population all-gather -> pair-sharded A-step -> rows gathered in CSR
+order must equal one rank doing everything.  The per-shard A-step
+compute here is the CPU oracle standing in for the HIP kernel (which the gpu
+tests check against the same oracle)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from conftest import GOLDEN, make_pairs
+from igm_amd import pipeline
+from igm_amd._lib import row_dtype
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _inputs():
+    pop = np.load(os.path.join(GOLDEN, 'demo_population.npz'))
+    hic = np.load(os.path.join(GOLDEN, 'demo_hic_pairs.npz'))
+    keep = np.where(hic['p'] >= 0.05)[0][:3001]
+    pairs = make_pairs(hic['i'][keep], hic['j'][keep], hic['p'][keep].astype(np.float64), np.zeros(len(keep)))
+    xyz_sm = np.ascontiguousarray(pop['coordinates'][:, :30].transpose(1, 0, 2))  # (S, nbead, 3) struct-major
+    return pop, pairs, xyz_sm
+
+
+def _worker(rank, world, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        pop, pairs, xyz_sm = _inputs()
+        S = xyz_sm.shape[0]
+        s0, s1 = pipeline.shard(S, rank, world)
+        local = torch.from_numpy(xyz_sm[s0:s1].copy())
+        full = pipeline.gather_population(local).numpy()
+        assert np.array_equal(full, xyz_sm)
+        bead_major = np.ascontiguousarray(full.transpose(1, 0, 2))
+        lo, hi = pipeline.shard(len(pairs), rank, world)
+        rows, _ = oracle.actdist(bead_major, pop['radii'], pop['copy_ptr'], pop['copy_idx'], pop['chrom'],
+                                 pairs[lo:hi], 2.0, 1)
+        u8 = torch.from_numpy(rows.view(np.uint8).copy())
+        allrows, n = pipeline.gather_rows(u8, len(rows), row_dtype.itemsize)
+        tot = pipeline.reduce_sum_f64([float(rank + 1), 2.0], torch.device('cpu'))
+        if rank == 0:
+            np.save(out, allrows.numpy())
+            assert n * row_dtype.itemsize == allrows.numel()
+            assert tot.tolist() == [3.0, 4.0]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_covers_everything():
+    for n in (0, 1, 7, 1000, 45123):
+        for world in (1, 2, 3, 8):
+            spans = [pipeline.shard(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[k][1] == spans[k + 1][0] for k in range(world - 1))
+
+
+def test_two_rank_astep_rows_equal_single_rank(tmp_path):
+    out = str(tmp_path / 'rows.npy')
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    pop, pairs, xyz_sm = _inputs()
+    ref, _ = oracle.actdist(np.ascontiguousarray(xyz_sm.transpose(1, 0, 2)), pop['radii'], pop['copy_ptr'],
+                            pop['copy_idx'], pop['chrom'], pairs, 2.0, 1)
+    assert got.tobytes() == ref.tobytes()
+    assert len(ref) > 500
