@@ -1,0 +1,69 @@
+"""Summarise rocprofv3 outputs (rocpd sqlite .db) of scripts/gpu_bench.sh into the
+text files committed under profiles/<tag>/.
+
+    python scripts/prof_summary.py gpurun_out/<tag> profiles/<tag>
+
+kernel_stats.txt   per kernel: calls, total/avg duration (--kernel-trace --stats run)
+hbm_traffic.txt    per kernel: FETCH_SIZE / WRITE_SIZE (separate --pmc runs), in KB as
+                   rocprofv3 reports them, and the HBM bytes per launch after the
+                   gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE x 2)
+"""
+import glob
+import os
+import sqlite3
+import sys
+
+
+def short(name, n=90):
+    name = name.split('(')[0] if not name.startswith('(') else name
+    return name if len(name) <= n else name[:n - 3] + '...'
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = list(c.execute('select name, count(*), sum(duration), avg(duration), max(grid_x / workgroup_x), '
+                          'max(workgroup_x), max(vgpr_count), max(lds_size) from kernels group by name '
+                          'order by 3 desc'))
+    total = sum(r[2] for r in rows) or 1
+    lines = ['%-90s %6s %14s %14s %7s %8s %5s %5s %7s' % ('kernel', 'calls', 'total_ms', 'avg_ms', 'pct', 'grid',
+                                                         'wg', 'vgpr', 'lds')]
+    for n, k, tot, avg, g, wg, vg, lds in rows:
+        lines.append('%-90s %6d %14.3f %14.3f %7.3f %8d %5d %5d %7d' % (short(n), k, tot * 1e-6, avg * 1e-6,
+                                                                       100.0 * tot / total, g, wg, vg, lds))
+    return lines
+
+
+def pmc(db):
+    c = sqlite3.connect(db)
+    q = ('select kernel_name, counter_name, count(*), sum(value), avg(end - start) from counters_collection '
+         'group by kernel_name, counter_name')
+    return list(c.execute(q))
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    for db in glob.glob(os.path.join(src, 'kt', '*.db')):
+        with open(os.path.join(dst, 'kernel_stats.txt'), 'w') as f:
+            f.write('# rocprofv3 --kernel-trace --stats, %s\n' % os.path.basename(db))
+            f.write('\n'.join(kernel_stats(db)) + '\n')
+    out = ['# PMC passes (one counter per rocprofv3 run). value_KB = rocprofv3 FETCH_SIZE/WRITE_SIZE summed over',
+           '# the launches; hbm_bytes_per_launch = KB*1024/calls, FETCH_SIZE doubled (gfx950 correction).',
+           '%-70s %-10s %6s %18s %22s %14s' % ('kernel', 'counter', 'calls', 'value_KB', 'hbm_bytes_per_launch',
+                                               'avg_ns')]
+    for sub in ('fetch', 'write'):
+        for db in glob.glob(os.path.join(src, sub, '*.db')):
+            for k, cn, n, v, dur in pmc(db):
+                corr = 2.0 if cn == 'FETCH_SIZE' else 1.0
+                out.append('%-70s %-10s %6d %18.1f %22.4g %14.0f' % (short(k, 70), cn, n, v, v * 1024 * corr / n,
+                                                                       dur))
+    with open(os.path.join(dst, 'hbm_traffic.txt'), 'w') as f:
+        f.write('\n'.join(out) + '\n')
+    for fn in ('bench.log', 'host.txt'):
+        p = os.path.join(src, fn)
+        if os.path.exists(p):
+            with open(p) as fi, open(os.path.join(dst, fn.replace('.log', '.jsonl')), 'w') as fo:
+                fo.write(''.join(l for l in fi if l.startswith('{') or fn == 'host.txt'))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], sys.argv[2])
