@@ -172,8 +172,11 @@ def main():
                           'violations_ms': it.ctx.kernel_ms('violations'),
                           'violation_score': score, 'median_final_energy_per_bead':
                               float(np.median(info['final_energy'])) / inp['atoms'].nbead,
-                          'rows': int(it.nrows), 'hic_bonds_per_struct': it.nbonds / it.S_local},
+                          'rows': int(it.nrows), 'hic_bonds_per_struct': it.nbonds / it.S_local,
+                          'mean_rebuilds': float(np.mean(info['nrebuild']))},
         }
+        if os.environ.get('IGM_PROF'):
+            line['profile'] = it.ctx.mstep_profile()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -23,6 +23,7 @@ IGM_E_UNSUPPORTED = -5
 IGM_DEVICE_PTRS = 0x1
 IGM_ASYNC = 0x2
 IGM_F32_PATH = 0x4
+IGM_MSTEP_FORCE_GLOBAL = 0x1  # igm_mstep_params.flags: HBM-resident kernels even when LDS fits
 
 IGM_MAX_STAGES = 16
 IGM_MAX_ENVELOPES = 4
@@ -90,6 +91,7 @@ SIGNATURES = {
     'igm_ctx_set_stream': (_i32, [_vp, _vp]),
     'igm_ctx_synchronize': (_i32, [_vp]),
     'igm_last_kernel_ms': (_f64, [_vp, ctypes.c_char_p]),
+    'igm_mstep_last_profile': (_i32, [_vp, _vp]),
     'igm_version': (ctypes.c_char_p, []),
     'igm_astep_actdist': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _f64, _i32,
                                  _vp, _vp, _i64, ctypes.POINTER(_i64)]),
@@ -169,6 +171,12 @@ class Context(object):
 
     def kernel_ms(self, name):
         return self.lib.igm_last_kernel_ms(self.h, name.encode())
+
+    def mstep_profile(self):
+        """cycle counters of the last anneal launch (IGM_PROF=1): dict of sums."""
+        out = (ctypes.c_ulonglong * 5)()
+        self.check(self.lib.igm_mstep_last_profile(self.h, out), 'igm_mstep_last_profile')
+        return dict(zip(('build_cycles', 'force_cycles', 'rest_cycles', 'evaluations', 'builds'), list(out)))
 
     def close(self):
         if getattr(self, 'h', None):

@@ -1,24 +1,32 @@
 // M-step engine: batched replacement of the per-structure serial LAMMPS run
 // (igm/model/kernel/lammps.py:361-492 via ModelingStep.task, ModelingStep.py:508-509).
 //
-// Design (MI355X-first, see DESIGN.md):
+// Design (MI355X-first, see DESIGN.md §4):
 //  * one workgroup = one structure, persistent: it pulls structure ids from an
 //    atomic work counter and runs the WHOLE protocol for that structure inside
 //    one launch (47 000 MD steps for the demo protocol) -- no per-step launches.
-//  * positions live in LDS (float4 x,y,z,radius); each thread owns BPT atoms
-//    (a = b*NT + tid) and keeps their velocity, force and last-build position in
+//  * LDS path (natom <= 3072, the 2 Mb diploid model): float4 positions
+//    (x, y, z, radius) AND the Verlet list live in LDS; each thread owns BPT atoms
+//    (a = b*NT + t) and keeps their velocity, force and last-build position in
 //    VGPRs.  Per MD step: one barrier after the position update (fused with the
 //    neighbour-displacement vote, __syncthreads_or) and one for the temperature
-//    reduction of fix temp/rescale.
-//  * neighbours: Verlet list with skin (LAMMPS 'neighbor maxrad bin', 'check yes'),
-//    rebuilt in-kernel from an LDS cell grid (count / scan / scatter / per-cell
-//    sort -> deterministic order) into a sliced-ELLPACK list in HBM
-//    ([slice][k][64 lanes], coalesced per k).
-//  * bonds: per-structure sliced-ELLPACK adjacency (both ends) built once by
-//    adj_count/adj_fill, sorted per atom for a fixed summation order.
+//    sum of fix temp/rescale.  The only per-step HBM/L2 traffic left is the
+//    compact bond adjacency (4 B per bond end).
+//  * HBM path (larger structures, the 200 kb model with 29 838 beads): the same
+//    algorithm with positions, Verlet list, cell grid and per-atom state in a
+//    per-workgroup HBM workspace (L2/MALL-resident working set).
+//  * neighbours: Verlet list with skin (LAMMPS 'neighbor maxrad bin', 'check
+//    yes'), rebuilt in-kernel from a cell grid (count / scan / scatter / per-cell
+//    sort -> deterministic order) into a compact CSR list (u16 entries).  Atoms
+//    past the list capacity take their pair forces by walking the 27 cells of the
+//    build-time grid, a superset of their list visited in the same order.
+//  * bonds: per-structure sliced-ELLPACK adjacency (both ends, per-atom sorted
+//    for a fixed summation order) of 4-byte entries j | type << 16 | lower << 31;
+//    (r0, k) come from the structure's bond-type table -- the bond types LAMMPS
+//    itself dedupes (lammps_model.py:314-329).
 //  * anneal (MD) in f32 with f64 reductions; the CG minimisation (LAMMPS
-//    min_style cg, quadratic line search) runs in a second kernel in f64 with
-//    f64 positions in LDS, because its energy tests (EMACH = 1e-8) need it.
+//    min_style cg, quadratic line search) runs in a second kernel in f64,
+//    because its energy tests (EMACH = 1e-8) need it.
 #include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
@@ -30,144 +38,275 @@ namespace igm {
 namespace ms {
 
 constexpr uint32_t kLowerBit = 0x80000000u;
-// nnb value of an atom with more list candidates than the capacity: its pair
-// forces are taken by walking the 27 cells of the build-time grid, which
-// visits a superset of its list in the same order (so no overflow error).
-constexpr int kNnbWalk = 0xFFFF;
-constexpr int kMaxTypes = 2048;  // distinct radii (LAMMPS atom types); the pair table is kMaxTypes^2
+constexpr int kNnbWalk = 0xFFFF;          // nnb of an atom whose pair forces come from a cell walk
+constexpr int kMaxTypes = 2048;           // distinct radii (LAMMPS atom types); the pair table is kMaxTypes^2
+constexpr int kTypeHash = 8192;           // LDS hash slots of the bond-type builder
+constexpr int kMaxBondTypes = 4096;       // distinct (r0, k) per structure
+constexpr int kCellCapBig = 32768;        // cell grid of an HBM-resident structure
+constexpr size_t kLdsBytes = 160 * 1024 - 1024;  // dynamic LDS per workgroup: 160 KB per CU (gfx950) less a static reserve
+constexpr int kNeighBudget = 64;          // default Verlet-list slots per atom
+constexpr int kLdsListSlots = 8;          // LDS path: the first slots of every atom's list live in LDS
+#ifndef IGM_PAIR_BATCH
+#define IGM_PAIR_BATCH 4
+#endif
+
+// ------------------------------------------------------------------ carving
+struct Carver {
+    unsigned char* base;
+    size_t o;
+    __host__ __device__ explicit Carver(void* b) : base(static_cast<unsigned char*>(b)), o(0) {}
+    template <typename T>
+    __host__ __device__ T* take(size_t n) {
+        o = (o + 15) & ~size_t(15);
+        T* p = reinterpret_cast<T*>(base + o);
+        o += n * sizeof(T);
+        return p;
+    }
+};
 
 struct Bonds {
-    const int4* ent;     // all structures' SELL entries
-    const int64_t* base; // (B) entry offset of structure s
-    const int* soff;     // (B, nslice+1) slice offsets (entries)
-    const int* deg;      // (B, natom)
+    const uint32_t* ent;   // compact entries, sliced ELLPACK [slice][k][64 lanes]
+    const int64_t* base;   // (B) first entry of structure s
+    const int* soff;       // (B, nslice+1) slice offsets (entries)
+    const int* deg;        // (B, natom)
+    const float2* types;   // (r0, k) of every structure's bond types
+    const int64_t* tbase;  // (B) first type of structure s
+    const int64_t* ntype;  // (B) bond types of structure s
+};
+
+// The bonds of one atom: either the HBM adjacency (g: ELLPACK entries, stride 64,
+// types gt) or, when the structure's bonds were staged in LDS, a CSR row l of u16
+// entries j | (2*type + lower) << 12 with the type table lt.
+struct BondView {
+    const uint32_t* g;
+    const float2* gt;
+    const uint16_t* l;
+    const float2* lt;
+    int n;
 };
 
 struct Common {
-    int nstruct, natom, nslice, kcap;
+    int nstruct, natom, nslice, ldn;  // ldn: SoA stride of per-atom HBM arrays (natom rounded to 64)
     const float* radii;
     const int* atype;  // per atom: index into DevParams::pair_tab / rtype
     const uint32_t* aflags;
     Bonds bonds;
     int* work_counter;  // dynamic structure scheduler
-    int* error;         // overflow flag (per launch)
+    int* error;         // error bits (per launch)
+    int kcap;           // Verlet-list slots per atom (LDS + HBM)
 };
 
-// ------------------------------------------------------------------ LDS carve
-// MD kernel (f32):  pos f4[npad] | frc f4[npad] | cell i32[kCellCap+4] | red 3x | wsum | misc |
-//                   nnb u16[npad] | sorted u16[npad] | slot u16[npad] | cellid u16[npad]
-// CG kernel (f64):  pos d4[npad] | ... same tail, forces live in HBM scratch.
-template <typename T>
-struct Smem {
-    vec4_t<T>* pos;
-    float4* frc;      // MD only
-    int* cell;        // kCellCap + 4
-    double* red0;     // kMaxWaves*8
+// the neighbour structure of one workgroup (pointers into LDS or HBM).  The Verlet
+// list is a fixed-capacity ELLPACK built in ONE pass: slot k < kl of atom a lives at
+// lell[k * lstride + a] (LDS, bank-conflict free), slot k >= kl at
+// gell[((a >> 6) * kg + k - kl) * 64 + (a & 63)] (HBM, one coalesced line per wave);
+// an atom with more than kl + kg neighbours takes its pair forces from a cell walk.
+template <typename T, typename OffT>
+struct NList {
+    OffT* cell;        // ncell+1 offsets into sorted (build-time cell grid)
+    uint16_t* sorted;  // bead ids by cell, ascending inside a cell
+    uint16_t* nnb;     // per atom: list length, or kNnbWalk
+    uint16_t* lell;
+    int lstride, kl;
+    uint16_t* gell;
+    int kg;
+    int* scratch;      // the build's int scratch: (ncell + 1) + natom ints (aliases a list region)
+    int cellcap;
+    T* gp;             // lo[3], inv[3] of the grid (LDS)
+    int* gn;           // nb[3] (LDS)
+    __device__ __forceinline__ uint16_t* slot(int a, int k) const {
+        return k < kl ? lell + (size_t)k * lstride + a : gell + ((size_t)(a >> 6) * kg + (k - kl)) * 64 + (a & 63);
+    }
+};
+
+// small LDS block shared by every kernel variant
+struct Red {
+    double* red0;  // kMaxWaves*8
     double* red1;
     double* redb;
-    int* wsum;        // kMaxWaves
-    int* misc;        // 16 ints
-    uint16_t* nnb;    // npad
-    uint16_t* sorted; // npad
-    uint16_t* slot;   // npad
-    uint16_t* cellid; // npad
+    int* wsum;     // kMaxWaves
+    int* misc;     // 16
 };
 
 template <typename T>
-__host__ __device__ inline size_t smem_bytes(int npad) {
-    size_t b = sizeof(vec4_t<T>) * (size_t)npad;
-    if (sizeof(T) == 4) b += sizeof(float4) * (size_t)npad;
-    b += sizeof(int) * (kCellCap + 4);
-    b += 3 * sizeof(double) * kMaxWaves * 8;
-    b += sizeof(int) * (kMaxWaves + 16);
-    b += 4 * ((sizeof(uint16_t) * (size_t)npad + 15) / 16) * 16;
-    return b;
+__host__ __device__ inline Red carve_red(Carver& cv, T** gp, int** gn) {
+    Red r;
+    r.red0 = cv.take<double>(kMaxWaves * 8);
+    r.red1 = cv.take<double>(kMaxWaves * 8);
+    r.redb = cv.take<double>(kMaxWaves * 8);
+    r.wsum = cv.take<int>(kMaxWaves);
+    r.misc = cv.take<int>(16);
+    *gp = cv.take<T>(8);
+    *gn = cv.take<int>(8);
+    return r;
 }
+
+// LDS layout of the MD kernel (LDS path).  `rest` holds the structure's bond CSR
+// (when it fits) followed by the Verlet list; the list also serves as the build's
+// int scratch.
+constexpr int kLdsBondTypes = 8;  // 3-bit type field of an LDS bond entry (x2 for the lower-bound bit)
+
+struct MdLds {
+    Red r;
+    float4* pos;
+    uint16_t* boff;  // npad+8 bond CSR offsets
+    float2* btab;    // kLdsBondTypes (r0, k)
+    uint16_t* rest;  // the structure's bond CSR, when it fits
+    int rest_cap;    // u16 entries
+    NList<float, uint16_t> L;
+};
+
+__host__ __device__ inline MdLds carve_md_lds(void* smem, int npad) {
+    Carver cv(smem);
+    MdLds m;
+    m.r = carve_red<float>(cv, &m.L.gp, &m.L.gn);
+    m.pos = cv.take<float4>(npad);
+    m.L.cell = cv.take<uint16_t>(kCellCap + 8);
+    m.L.nnb = cv.take<uint16_t>(npad);
+    m.L.sorted = cv.take<uint16_t>(npad);
+    m.boff = cv.take<uint16_t>(npad + 8);
+    m.btab = cv.take<float2>(kLdsBondTypes);
+    m.L.lell = cv.take<uint16_t>((size_t)kLdsListSlots * npad);
+    m.L.lstride = npad;
+    m.L.kl = kLdsListSlots;
+    m.L.scratch = reinterpret_cast<int*>(m.L.lell);
+    m.L.gell = nullptr;
+    m.L.kg = 0;
+    m.L.cellcap = kCellCap;
+    m.rest = cv.take<uint16_t>(0);
+    const long rest = (long)kLdsBytes - (long)cv.o;
+    m.rest_cap = rest > 0 ? (int)(rest / 2) : 0;
+    return m;
+}
+
+// ints of the build's scratch: (ncell + 1) counts + natom slots
+__host__ __device__ inline size_t build_scratch_bytes(int cellcap, int natom) {
+    return sizeof(int) * (size_t)(cellcap + 2 + natom);
+}
+
+// HBM workspace of one workgroup: the neighbour structure (both kernels) and,
+// for the MD kernel of the HBM path, positions + per-atom state
+template <typename T>
+struct BigWs {
+    vec4_t<T>* pos;
+    T* v;   // [3][ldn]
+    T* f;   // [3][ldn]
+    T* xb;  // [3][ldn]
+};
 
 template <typename T>
-__device__ inline Smem<T> carve(unsigned char* smem, int npad) {
-    Smem<T> s;
-    size_t o = 0;
-    s.pos = reinterpret_cast<vec4_t<T>*>(smem + o);
-    o += sizeof(vec4_t<T>) * (size_t)npad;
-    s.frc = nullptr;
-    if (sizeof(T) == 4) {
-        s.frc = reinterpret_cast<float4*>(smem + o);
-        o += sizeof(float4) * (size_t)npad;
-    }
-    s.red0 = reinterpret_cast<double*>(smem + o);
-    o += sizeof(double) * kMaxWaves * 8;
-    s.red1 = reinterpret_cast<double*>(smem + o);
-    o += sizeof(double) * kMaxWaves * 8;
-    s.redb = reinterpret_cast<double*>(smem + o);
-    o += sizeof(double) * kMaxWaves * 8;
-    s.cell = reinterpret_cast<int*>(smem + o);
-    o += sizeof(int) * (kCellCap + 4);
-    s.wsum = reinterpret_cast<int*>(smem + o);
-    o += sizeof(int) * kMaxWaves;
-    s.misc = reinterpret_cast<int*>(smem + o);
-    o += sizeof(int) * 16;
-    const size_t u16b = ((sizeof(uint16_t) * (size_t)npad + 15) / 16) * 16;
-    s.nnb = reinterpret_cast<uint16_t*>(smem + o);
-    o += u16b;
-    s.sorted = reinterpret_cast<uint16_t*>(smem + o);
-    o += u16b;
-    s.slot = reinterpret_cast<uint16_t*>(smem + o);
-    o += u16b;
-    s.cellid = reinterpret_cast<uint16_t*>(smem + o);
-    return s;
+__host__ __device__ inline size_t carve_ws(void* base, int natom, int ldn, int kg, int cellcap, bool with_pos,
+                                           bool with_state, NList<T, int>* L, BigWs<T>* W) {
+    Carver cv(base);
+    L->cell = cv.take<int>(cellcap + 8);
+    L->nnb = cv.take<uint16_t>(ldn);
+    L->sorted = cv.take<uint16_t>(ldn);
+    L->gell = cv.take<uint16_t>((size_t)ldn * kg);
+    L->kg = kg;
+    L->lell = nullptr;
+    L->lstride = 0;
+    L->kl = 0;
+    L->scratch = reinterpret_cast<int*>(L->gell);
+    L->cellcap = cellcap;
+    W->pos = with_pos ? cv.take<vec4_t<T>>(ldn) : nullptr;
+    W->v = with_state ? cv.take<T>(3 * (size_t)ldn) : nullptr;
+    W->f = with_state ? cv.take<T>(3 * (size_t)ldn) : nullptr;
+    W->xb = with_state ? cv.take<T>(3 * (size_t)ldn) : nullptr;
+    return (cv.o + 255) & ~size_t(255);
 }
 
-// --------------------------------------------------------- neighbour build
-template <int NT>
-__device__ __forceinline__ void block_exclusive_scan(int* a, int n, int* wsum) {
+// --------------------------------------------------------- block scans
+// out[i] = sum_{k<i} in[k] (i < n), out[n] = total; in may alias out.  Stored
+// values saturate at the range of OutT (u16 offsets past the LDS list capacity
+// only need to compare >= it).
+template <int NT, typename InT, typename OutT>
+__device__ __forceinline__ void block_scan(const InT* in, OutT* out, int n, int* wsum) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int cpt = (n + NT - 1) / NT;
     const int beg = t * cpt;
-    int s = 0;
+    constexpr long kMax = sizeof(OutT) == 2 ? 0xFFFF : 0x7FFFFFFF;
+    long s = 0;
     for (int i = 0; i < cpt; ++i) {
         const int idx = beg + i;
-        if (idx < n) {
-            const int v = a[idx];
-            a[idx] = s;
-            s += v;
-        }
+        if (idx < n) s += (long)in[idx];
     }
-    int incl = s;
+    long incl = s;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off);
+        const long y = __shfl_up(incl, off);
         if (lane >= off) incl += y;
     }
-    if (lane == 63) wsum[w] = incl;
+    if (lane == 63) wsum[w] = (int)(incl > 0x7FFFFFFF ? 0x7FFFFFFF : incl);
     __syncthreads();
-    int woff = 0, total = 0;
+    long woff = 0, total = 0;
     for (int i = 0; i < NT / 64; ++i) {
         if (i < w) woff += wsum[i];
         total += wsum[i];
     }
-    const int toff = woff + incl - s;
+    long run = woff + incl - s;
     for (int i = 0; i < cpt; ++i) {
         const int idx = beg + i;
-        if (idx < n) a[idx] += toff;
+        if (idx < n) {
+            const long v = (long)in[idx];
+            out[idx] = (OutT)(run < kMax ? run : kMax);
+            run += v;
+        }
     }
-    if (t == 0) a[n] = total;
+    if (t == 0) out[n] = (OutT)(total < kMax ? total : kMax);
     __syncthreads();
 }
 
-// Verlet list with skin from an LDS cell grid.  Positions are read from sm.pos
-// (all writers have passed a barrier).  The bead mask is pos.w >= 0.
-template <typename T, int NT, int BPT>
-__device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, int kcap, T cut_list, int* error) {
+// --------------------------------------------------------- neighbour build
+template <typename T>
+__device__ __forceinline__ int cell_index(T x, T y, T z, const T* lo, const T* inv, const int* nb) {
+    const T pp[3] = {x, y, z};
+    int ci[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const int v = (int)((pp[d] - lo[d]) * inv[d]);
+        ci[d] = v < 0 ? 0 : (v >= nb[d] ? nb[d] - 1 : v);
+    }
+    return (ci[2] * nb[1] + ci[1]) * nb[0] + ci[0];
+}
+
+// visit the beads of the 27 cells around cell c (x-runs are contiguous in `sorted`):
+// f(j, valid) in batches of 4 -- the bead ids of a batch are loaded together so the
+// dependent LDS reads overlap; an invalid slot carries a valid id (masked by caller)
+template <typename OffT, typename F>
+__device__ __forceinline__ void walk27(int c, const OffT* cell, const uint16_t* sorted, const int* gn, F&& f) {
+    const int nx = gn[0], ny = gn[1], nz = gn[2];
+    const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+    for (int dz = -1; dz <= 1; ++dz) {
+        const int z0 = cz + dz;
+        if (z0 < 0 || z0 >= nz) continue;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int y0 = cy + dy;
+            if (y0 < 0 || y0 >= ny) continue;
+            const int row = (z0 * ny + y0) * nx;
+            const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
+            const int beg = (int)cell[row + xlo], end = (int)cell[row + xhi + 1];
+            for (int q = beg; q < end; q += 4) {
+                int jj[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) jj[u] = (int)sorted[q + u < end ? q + u : beg];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) f(jj[u], q + u < end);
+            }
+        }
+    }
+}
+
+// Verlet list with skin from a cell grid.  Positions are read from `pos` (all
+// writers have passed a barrier).  The bead mask is pos.w >= 0.  Ends with a
+// barrier.
+template <typename T, int NT, typename OffT>
+__device__ __noinline__ void build_nlist(int natom, const vec4_t<T>* pos, NList<T, OffT> L, T cut_list, Red R) {
     const int t = threadIdx.x;
-    const int lane = t & 63;
     float mm[6];
 #pragma unroll
     for (int d = 0; d < 6; ++d) mm[d] = -3.0e38f;
-    for (int b = 0; b < BPT; ++b) {
-        const int a = b * NT + t;
-        if (a >= natom) break;
-        const vec4_t<T> p = sm.pos[a];
+    for (int a = t; a < natom; a += NT) {
+        const vec4_t<T> p = pos[a];
         if (!(p.w >= T(0))) continue;
         mm[0] = fmaxf(mm[0], -(float)p.x);
         mm[1] = fmaxf(mm[1], -(float)p.y);
@@ -180,11 +319,11 @@ __device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, i
         double md[6];
 #pragma unroll
         for (int d = 0; d < 6; ++d) md[d] = mm[d];
-        block_max<NT, 6>(md, sm.redb);
+        block_max<NT, 6>(md, R.redb);
 #pragma unroll
         for (int d = 0; d < 6; ++d) mm[d] = (float)md[d];
     }
-    // grid (identical in every thread): cells of side >= cut_list, at most kCellCap
+    // grid (identical in every thread): cells of side >= cut_list, at most cellcap
     T lo[3], inv[3];
     int nb[3];
     {
@@ -192,13 +331,12 @@ __device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, i
         const float cut = (float)cut_list;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            // bounding box with a 1 ulp-safe margin (f32 min/max of f64 positions)
             ext[d] = mm[3 + d] + mm[d];
             if (!(ext[d] >= 0.0f)) ext[d] = 0.0f;
             vol *= fmaxf(ext[d], cut);
         }
         float cs = cut;
-        if (vol / (cs * cs * cs) > (float)kCellCap) cs = cbrtf(vol / (float)kCellCap) * 1.0001f;
+        if (vol / (cs * cs * cs) > (float)L.cellcap) cs = cbrtf(vol / (float)L.cellcap) * 1.0001f;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             lo[d] = (T)(-mm[d]);
@@ -208,91 +346,68 @@ __device__ __noinline__ void build_nlist(int natom, Smem<T> sm, uint16_t* nbr, i
         }
     }
     const int ncell = nb[0] * nb[1] * nb[2];
-    if (t == 0) {  // for the cell walk of atoms past the list capacity (before the barrier below)
-        sm.misc[4] = nb[0];
-        sm.misc[5] = nb[1];
-        sm.misc[6] = nb[2];
-    }
-    for (int c = t; c <= ncell; c += NT) sm.cell[c] = 0;
-    __syncthreads();
-    for (int b = 0; b < BPT; ++b) {
-        const int a = b * NT + t;
-        if (a >= natom) break;
-        const vec4_t<T> p = sm.pos[a];
-        if (!(p.w >= T(0))) continue;
-        const T pp[3] = {p.x, p.y, p.z};
-        int ci[3];
+    if (t == 0) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            const int v = (int)((pp[d] - lo[d]) * inv[d]);
-            ci[d] = v < 0 ? 0 : (v >= nb[d] ? nb[d] - 1 : v);
+            L.gp[d] = lo[d];
+            L.gp[3 + d] = inv[d];
+            L.gn[d] = nb[d];
         }
-        const int c = (ci[2] * nb[1] + ci[1]) * nb[0] + ci[0];
-        sm.cellid[a] = (uint16_t)c;
-        sm.slot[a] = (uint16_t)atomicAdd(&sm.cell[c], 1);
+    }
+    int* cnt = L.scratch;  // ncell+1 counts, then natom slots
+    int* slot = cnt + ncell + 1;
+    for (int c = t; c <= ncell; c += NT) cnt[c] = 0;
+    __syncthreads();
+    for (int a = t; a < natom; a += NT) {
+        const vec4_t<T> p = pos[a];
+        if (!(p.w >= T(0))) continue;
+        slot[a] = atomicAdd(&cnt[cell_index<T>(p.x, p.y, p.z, lo, inv, nb)], 1);
     }
     __syncthreads();
-    block_exclusive_scan<NT>(sm.cell, ncell, sm.wsum);
-    for (int b = 0; b < BPT; ++b) {
-        const int a = b * NT + t;
-        if (a >= natom) break;
-        if (!(sm.pos[a].w >= T(0))) continue;
-        sm.sorted[sm.cell[sm.cellid[a]] + sm.slot[a]] = (uint16_t)a;
+    block_scan<NT, int, int>(cnt, cnt, ncell, R.wsum);
+    for (int c = t; c <= ncell; c += NT) L.cell[c] = (OffT)cnt[c];
+    for (int a = t; a < natom; a += NT) {
+        const vec4_t<T> p = pos[a];
+        if (!(p.w >= T(0))) continue;
+        L.sorted[cnt[cell_index<T>(p.x, p.y, p.z, lo, inv, nb)] + slot[a]] = (uint16_t)a;
     }
     __syncthreads();
     for (int c = t; c < ncell; c += NT) {  // deterministic order inside each cell
-        const int beg = sm.cell[c], end = sm.cell[c + 1];
+        const int beg = (int)L.cell[c], end = (int)L.cell[c + 1];
         for (int i = beg + 1; i < end; ++i) {
-            const uint16_t v = sm.sorted[i];
+            const uint16_t v = L.sorted[i];
             int k = i - 1;
-            while (k >= beg && sm.sorted[k] > v) {
-                sm.sorted[k + 1] = sm.sorted[k];
+            while (k >= beg && L.sorted[k] > v) {
+                L.sorted[k + 1] = L.sorted[k];
                 --k;
             }
-            sm.sorted[k + 1] = v;
+            L.sorted[k + 1] = v;
         }
     }
     __syncthreads();
-    (void)error;
     const T cut2 = cut_list * cut_list;
-    for (int b = 0; b < BPT; ++b) {
-        const int a = b * NT + t;
-        if (a >= natom) break;
-        const vec4_t<T> p0 = sm.pos[a];
-        int cnt = 0;
+    // one pass: walk the 27 cells, write the list slots (the scratch above is dead)
+    const int cap = L.kl + L.kg;
+    for (int a = t; a < natom; a += NT) {
+        const vec4_t<T> p0 = pos[a];
+        int k = 0;
         if (p0.w >= T(0)) {
-            uint16_t* out = nbr + (size_t)(a >> 6) * kcap * 64 + lane;
-            const int c = sm.cellid[a];
-            const int cx = c % nb[0], cy = (c / nb[0]) % nb[1], cz = c / (nb[0] * nb[1]);
-            for (int dz = -1; dz <= 1; ++dz) {
-                const int z0 = cz + dz;
-                if (z0 < 0 || z0 >= nb[2]) continue;
-                for (int dy = -1; dy <= 1; ++dy) {
-                    const int y0 = cy + dy;
-                    if (y0 < 0 || y0 >= nb[1]) continue;
-                    const int row = (z0 * nb[1] + y0) * nb[0];
-                    const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nb[0] ? cx + 1 : nb[0] - 1;
-                    const int beg = sm.cell[row + xlo], end = sm.cell[row + xhi + 1];  // contiguous x-run
-                    for (int q = beg; q < end; ++q) {
-                        const int j = sm.sorted[q];
-                        if (j == a) continue;
-                        const vec4_t<T> p = sm.pos[j];
-                        const T ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
-                        if (ddx * ddx + ddy * ddy + ddz * ddz < cut2) {
-                            if (cnt < kcap) out[(size_t)cnt * 64] = (uint16_t)j;
-                            ++cnt;
-                        }
-                    }
-                }
-            }
-            if (cnt > kcap) cnt = kNnbWalk;  // the force routine walks the cells instead
+            walk27(cell_index<T>(p0.x, p0.y, p0.z, lo, inv, nb), L.cell, L.sorted, nb, [&](int j, bool ok) {
+                const vec4_t<T> p = pos[j];
+                const T ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
+                const bool in = ok && j != a && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
+                if (in && k < L.kl) L.lell[(size_t)k * L.lstride + a] = (uint16_t)j;
+                if (in && k >= L.kl && k < cap) L.gell[((size_t)(a >> 6) * L.kg + (k - L.kl)) * 64 + (a & 63)] = (uint16_t)j;
+                k += in ? 1 : 0;
+            });
         }
-        sm.nnb[a] = (uint16_t)cnt;
+        L.nnb[a] = (uint16_t)(k <= cap ? k : kNnbWalk);
     }
+    __syncthreads();
 }
 
 // ------------------------------------------------------------- forces
-// force (and energy if EN) on atom a; position p0 (w: f32 radius / f64 atom type, <0: no pair)
+// pair force (and energy if EN) of atom i (xi, yi, zi, radius/type ri) from atom j
 template <typename T, bool EN>
 __device__ __forceinline__ void pair_one(int j, T xi, T yi, T zi, T ri, const vec4_t<T>* pos, const DevParams& P,
                                          T evf, T& fx, T& fy, T& fz, double& ep) {
@@ -312,88 +427,129 @@ __device__ __forceinline__ void pair_one(int j, T xi, T yi, T zi, T ri, const ve
     if (EN) ep += 0.5 * e;
 }
 
-// the build-time cell grid (LDS), used for atoms past the list capacity
-struct CellGrid {
-    const int* cell;
-    const uint16_t* sorted;
-    const uint16_t* cellid;
-    const int* dims;  // sm.misc + 4
-};
-
-template <typename T, bool EN>
-__device__ __noinline__ void pair_walk(int a, T xi, T yi, T zi, T ri, const vec4_t<T>* pos, CellGrid g,
-                                       const DevParams& P, T evf, T* f, double* ep) {
-    const int nx = g.dims[0], ny = g.dims[1], nz = g.dims[2];
-    const int c = g.cellid[a];
-    const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
-    T fx = f[0], fy = f[1], fz = f[2];
-    double e = *ep;
-    for (int dz = -1; dz <= 1; ++dz) {
-        const int z0 = cz + dz;
-        if (z0 < 0 || z0 >= nz) continue;
-        for (int dy = -1; dy <= 1; ++dy) {
-            const int y0 = cy + dy;
-            if (y0 < 0 || y0 >= ny) continue;
-            const int row = (z0 * ny + y0) * nx;
-            const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
-            const int beg = g.cell[row + xlo], end = g.cell[row + xhi + 1];
-            for (int q = beg; q < end; ++q) {
-                const int j = g.sorted[q];
-                if (j != a) pair_one<T, EN>(j, xi, yi, zi, ri, pos, P, evf, fx, fy, fz, e);
-            }
-        }
-    }
-    f[0] = fx;
-    f[1] = fy;
-    f[2] = fz;
-    *ep = e;
+// pair forces of an atom past the list capacity: walk the 27 cells around its
+// build-time position (a superset of its list, visited in the same order)
+template <typename T, bool EN, typename OffT>
+__device__ __noinline__ void pair_walk(int a, T xi, T yi, T zi, T ri, const vec4_t<T>* pos, const NList<T, OffT>& L,
+                                       T bx, T by, T bz, const DevParams& P, T evf, T& fx, T& fy, T& fz,
+                                       double& ep) {
+    T gx = 0, gy = 0, gz = 0;
+    double e = 0.0;
+    walk27(cell_index<T>(bx, by, bz, L.gp, L.gp + 3, L.gn), L.cell, L.sorted, L.gn, [&](int j, bool ok) {
+        if (ok && j != a) pair_one<T, EN>(j, xi, yi, zi, ri, pos, P, evf, gx, gy, gz, e);
+    });
+    fx = gx;
+    fy = gy;
+    fz = gz;
+    if (EN) ep += e;
 }
 
-template <typename T, bool EN>
+// Total force on atom a, gathered by its owner thread: pairs from the Verlet
+// list (or the cell walk around the build-time position b*), bonds B, envelopes.
+template <typename T, bool EN, typename OffT>
 __device__ __forceinline__ void atom_force(int a, const vec4_t<T>& p0, uint32_t fl, const vec4_t<T>* pos,
-                                           const uint16_t* nl, int nn, const int4* al, int nd, const DevParams& P,
-                                           CellGrid grid, T evf, T envf, T& fx, T& fy, T& fz, double& ep,
-                                           double& eb, double (&ee)[IGM_MAX_ENVELOPES]) {
+                                           const NList<T, OffT>& L, T bx, T by, T bz, const BondView& B,
+                                           const DevParams& P, T evf, T envf, T& fx, T& fy,
+                                           T& fz, double& ep, double& eb, double (&ee)[IGM_MAX_ENVELOPES]) {
     fx = fy = fz = T(0);
     const T xi = p0.x, yi = p0.y, zi = p0.z;
     const T ri = (T)p0.w;
-    constexpr int U = 8;  // neighbour indices fetched per batch: one memory wait per U pairs
-    if (ri >= T(0) && nn == kNnbWalk) {
-        T f3[3] = {T(0), T(0), T(0)};
-        double e = 0.0;
-        pair_walk<T, EN>(a, xi, yi, zi, ri, pos, grid, P, evf, f3, &e);
-        fx = f3[0];
-        fy = f3[1];
-        fz = f3[2];
-        if (EN) ep += e;
-    } else if (ri >= T(0)) {
-        for (int k0 = 0; k0 < nn; k0 += U) {
-            int jv[U];
+    if (ri >= T(0)) {
+        const int nn = L.nnb[a];
+        if (nn == kNnbWalk) {
+            pair_walk<T, EN, OffT>(a, xi, yi, zi, ri, pos, L, bx, by, bz, P, evf, fx, fy, fz, ep);
+        } else if (nn > 0) {
+            // the LDS slots, then the HBM slots, in batches whose loads are all in flight together
+            constexpr int U = IGM_PAIR_BATCH;
+            const int n1 = nn < L.kl ? nn : L.kl;
+            const uint16_t* gl = L.gell + (size_t)(a >> 6) * L.kg * 64 + (a & 63);
+            if constexpr (std::is_same<T, float>::value) {
+                // one batch of U neighbours of a slot sequence idx(k), k < n (tail masked)
+                auto batch = [&](int k0, int n, auto idx) {
+                    int jv[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) jv[u] = (k0 + u < nn) ? (int)nl[(size_t)(k0 + u) * 64] : -1;
+                    for (int u = 0; u < U; ++u) jv[u] = (int)idx(k0 + u < n ? k0 + u : n - 1);
+                    float4 pj[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (jv[u] >= 0) pair_one<T, EN>(jv[u], xi, yi, zi, ri, pos, P, evf, fx, fy, fz, ep);
+                    for (int u = 0; u < U; ++u) pj[u] = pos[jv[u]];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const float dx = xi - pj[u].x, dy = yi - pj[u].y, dz = zi - pj[u].z;
+                        const float fp = soft_pair_bf(dx * dx + dy * dy + dz * dz, ri + pj[u].w, evf);
+                        const float m = (k0 + u < n) ? fp : 0.0f;
+                        fx += m * dx;
+                        fy += m * dy;
+                        fz += m * dz;
+                    }
+                };
+                const uint16_t* ll = L.lell + a;
+                const int ls = L.lstride;
+                for (int k0 = 0; k0 < n1; k0 += U) batch(k0, n1, [&](int k) { return ll[(size_t)k * ls]; });
+                const int n2 = nn - n1;
+                for (int k0 = 0; k0 < n2; k0 += U) batch(k0, n2, [&](int k) { return gl[(size_t)k * 64]; });
+            } else {
+                for (int k0 = 0; k0 < nn; k0 += U) {
+                    int jv[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int k = k0 + u;
+                        jv[u] = k >= nn ? -1 : (k < n1 ? (int)L.lell[(size_t)k * L.lstride + a] : (int)gl[(size_t)(k - n1) * 64]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (jv[u] >= 0) pair_one<T, EN>(jv[u], xi, yi, zi, ri, pos, P, evf, fx, fy, fz, ep);
+                }
+            }
         }
     }
-    constexpr int UB = 4;  // bond entries (16 B) per batch
-    for (int k0 = 0; k0 < nd; k0 += UB) {
-        int4 ev[UB];
+    if (B.l && B.n > 0) {
+        constexpr int UL = 4;  // LDS bond entries per batch, branch-free
+        for (int k0 = 0; k0 < B.n; k0 += UL) {
+            uint32_t ev[UL];
 #pragma unroll
-        for (int u = 0; u < UB; ++u) ev[u] = (k0 + u < nd) ? al[(size_t)(k0 + u) * 64] : make_int4(-1, 0, 0, 0);
+            for (int u = 0; u < UL; ++u) ev[u] = (uint32_t)B.l[k0 + u < B.n ? k0 + u : B.n - 1];
+            float2 rk[UL];
+            vec4_t<T> pj[UL];
 #pragma unroll
-        for (int u = 0; u < UB; ++u) {
-            if (k0 + u >= nd) continue;
-            const uint32_t jj = (uint32_t)ev[u].x;
-            const vec4_t<T> p = pos[jj & 0x7fffffffu];
-            const T dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
-            double e = 0.0;
-            const T fb = bond_term<T, EN>(dx * dx + dy * dy + dz * dz, (T)__int_as_float(ev[u].y),
-                                          (T)__int_as_float(ev[u].z), (jj & kLowerBit) != 0u, e);
-            fx += fb * dx;
-            fy += fb * dy;
-            fz += fb * dz;
-            if (EN) eb += 0.5 * e;
+            for (int u = 0; u < UL; ++u) {
+                rk[u] = B.lt[ev[u] >> 13];
+                pj[u] = pos[ev[u] & 0xfffu];
+            }
+#pragma unroll
+            for (int u = 0; u < UL; ++u) {
+                const T dx = xi - pj[u].x, dy = yi - pj[u].y, dz = zi - pj[u].z;
+                double e = 0.0;
+                const T fb = bond_term_bf<T, EN>(dx * dx + dy * dy + dz * dz, (T)rk[u].x, (T)rk[u].y,
+                                                 ((ev[u] >> 12) & 1u) != 0u, e);
+                const T m = (k0 + u < B.n) ? fb : T(0);
+                fx += m * dx;
+                fy += m * dy;
+                fz += m * dz;
+                if (EN && k0 + u < B.n) eb += 0.5 * e;
+            }
+        }
+    } else if (B.l) {
+    } else {
+        constexpr int UB = 4;  // HBM bond entries per batch
+        for (int k0 = 0; k0 < B.n; k0 += UB) {
+            uint32_t ev[UB];
+#pragma unroll
+            for (int u = 0; u < UB; ++u) ev[u] = (k0 + u < B.n) ? B.g[(size_t)(k0 + u) * 64] : 0u;
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                if (k0 + u >= B.n) continue;
+                const uint32_t e32 = ev[u];
+                const float2 rk = B.gt[(e32 >> 16) & 0x7fffu];
+                const vec4_t<T> p = pos[e32 & 0xffffu];
+                const T dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
+                double e = 0.0;
+                const T fb =
+                    bond_term<T, EN>(dx * dx + dy * dy + dz * dz, (T)rk.x, (T)rk.y, (e32 & kLowerBit) != 0u, e);
+                fx += fb * dx;
+                fy += fb * dy;
+                fz += fb * dz;
+                if (EN) eb += 0.5 * e;
+            }
         }
     }
     // non-bead atoms carry -(w + 1); f32: w = radius, f64: w = atom type
@@ -423,9 +579,10 @@ struct AnnealArgs {
     float* xyz;          // (B, natom, 3)
     float* vel;          // (B, natom, 3): out (mode 0) / in-out (mode 1)
     const float* vinit;  // mode 0: (B, nseg, natom, 3) velocities of each 'velocity create'
-    uint16_t* nbr_ws;    // per resident workgroup
-    size_t nbr_stride;
+    unsigned char* ws;   // HBM path: per resident workgroup
+    size_t ws_stride;
     int* nrebuild;       // (B)
+    unsigned long long* prof;  // optional: cycles {build, force, rest, steps, builds} summed over structures
     float* forces_out;   // forces at the end (B, natom, 3), may be null
     int mode;            // 0: full protocol, 1: one MD segment from vel
     int nseg;
@@ -436,20 +593,73 @@ struct AnnealArgs {
     float dt, t_window, t_fraction;
 };
 
+// next structure id of this workgroup (uniform), or >= nstruct when done
+__device__ __forceinline__ int next_structure(const Common& cm, int* misc) {
+    if (threadIdx.x == 0) misc[0] = atomicAdd(cm.work_counter, 1);
+    __syncthreads();
+    const int s = __builtin_amdgcn_readfirstlane(misc[0]);  // uniform: keeps derived pointers in SGPRs
+    __syncthreads();
+    return s;
+}
+
+// fix temp/rescale 1 t0 t1 window fraction at the end of step `step` of nsteps:
+// the factor applied to every velocity (1 if no rescale)
+__device__ __forceinline__ float temp_rescale_factor(double ke2, double dof, int step, int nsteps, float t0, float t1,
+                                                     float window, float fraction) {
+    const double tcur = dof > 0 ? ke2 / dof : 0.0;
+    if (!(tcur > 0.0)) return 1.0f;
+    const double delta = (double)step / (double)nsteps;
+    double tt = (double)t0 + delta * ((double)t1 - (double)t0);
+    if (!(fabs(tcur - tt) > (double)window)) return 1.0f;
+    tt = tcur - (double)fraction * (tcur - tt);
+    return (float)sqrt(tt / tcur);
+}
+
+// fix nve/limit half-kick with the velocity cap
+__device__ __forceinline__ void kick_limit(float& vx, float& vy, float& vz, float fx, float fy, float fz, float dtf,
+                                           float vlim, float vlimsq) {
+    vx += dtf * fx;
+    vy += dtf * fy;
+    vz += dtf * fz;
+    const float vsq = vx * vx + vy * vy + vz * vz;
+    if (vsq > vlimsq) {
+        const float sc = vlim * __frsqrt_rn(vsq);
+        vx *= sc;
+        vy *= sc;
+        vz *= sc;
+    }
+}
+
+// element b (runtime, uniform per loop trip) of a per-thread register array
+template <int BPT, typename X>
+__device__ __forceinline__ X pick(const X (&arr)[BPT], int b) {
+    X r = arr[0];
+#pragma unroll
+    for (int i = 1; i < BPT; ++i)
+        if (b == i) r = arr[i];
+    return r;
+}
+template <int BPT>
+__device__ __forceinline__ float pick(const float (&arr)[BPT][3], int b, int d) {
+    float r = arr[0][d];
+#pragma unroll
+    for (int i = 1; i < BPT; ++i)
+        if (b == i) r = arr[i][d];
+    return r;
+}
+
 template <int NT, int BPT>
 __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int npad = NT * BPT;
-    Smem<float> sm = carve<float>(smem, npad);
+    MdLds sm = carve_md_lds(smem, npad);
+    sm.L.gell = reinterpret_cast<uint16_t*>(A.ws + (size_t)blockIdx.x * A.ws_stride);  // list overflow (HBM)
+    sm.L.kg = A.cm.kcap - kLdsListSlots;
     const int t = threadIdx.x, lane = t & 63;
     const int natom = A.cm.natom;
-    uint16_t* nbr = A.nbr_ws + (size_t)blockIdx.x * A.nbr_stride;
-    float v[BPT][3], xb[BPT][3];
+    float v[BPT][3], f[BPT][3], xb[BPT][3];
     for (;;) {
-        if (t == 0) sm.misc[0] = atomicAdd(A.cm.work_counter, 1);
-        __syncthreads();
-        const int s = sm.misc[0];
-        __syncthreads();
+        const int s = next_structure(A.cm, sm.r.misc);
         if (s >= A.cm.nstruct) break;
         const float* xs = A.xyz + (size_t)s * natom * 3;
         uint32_t mobile = 0u;  // bit b: atom b*NT+t is integrated
@@ -467,21 +677,43 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
             const float r = in ? A.cm.radii[a] : 0.0f;
             sm.pos[a] = make_float4(in ? xs[(size_t)a * 3] : 0.f, in ? xs[(size_t)a * 3 + 1] : 0.f,
                                     in ? xs[(size_t)a * 3 + 2] : 0.f, bead ? r : -(r + 1.0f));
-            sm.frc[a] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
                 v[b][d] = 0.0f;
+                f[b][d] = 0.0f;
                 xb[b][d] = __int_as_float(0x7f800000);  // +inf: forces the first neighbour build
             }
         }
         double cnt[1] = {(double)nmob};
-        block_sum<NT, 1>(cnt, sm.red0);
+        block_sum<NT, 1>(cnt, sm.r.red0);
         const double dof = 3.0 * cnt[0] - 3.0;  // compute temp of group nonfixed
         __syncthreads();
-        const int4* adj = A.cm.bonds.ent + A.cm.bonds.base[s];
+        const uint32_t* adj = A.cm.bonds.ent + A.cm.bonds.base[s];
         const int* soff = A.cm.bonds.soff + (size_t)s * (A.cm.nslice + 1);
         const int* deg = A.cm.bonds.deg + (size_t)s * natom;
+        const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
+        // stage the bonds in LDS when the structure's types and entries fit: CSR of
+        // u16 entries j | (2*type + lower) << 12 ahead of the Verlet list
+        block_scan<NT, int, uint16_t>(deg, sm.boff, natom, sm.r.wsum);
+        const int nbent = __builtin_amdgcn_readfirstlane((int)sm.boff[natom]);
+        const int bond_u16 = (nbent + 7) & ~7;
+        const bool lds_bonds = A.cm.bonds.ntype[s] <= kLdsBondTypes && nbent < 0xFFFF && bond_u16 <= sm.rest_cap;
+        if (lds_bonds) {
+            for (int i = t; i < (int)A.cm.bonds.ntype[s]; i += NT) sm.btab[i] = bt[i];
+            for (int a = t; a < natom; a += NT) {
+                const uint32_t* g = adj + soff[a >> 6] + (a & 63);
+                uint16_t* o = sm.rest + sm.boff[a];
+                const int n = deg[a];
+                for (int k = 0; k < n; ++k) {
+                    const uint32_t e = g[(size_t)k * 64];
+                    o[k] = (uint16_t)((e & 0xfffu) | ((((e >> 16) & 0x7fffu) * 2u + (e >> 31)) << 12));
+                }
+            }
+        }
+        __syncthreads();
         int nbuild = 0;
+        unsigned long long c_build = 0, c_force = 0, c_all = 0, nstep_total = 0;
+        const unsigned long long c_begin = A.prof ? clock64() : 0;
         for (int seg = 0; seg < A.nseg; ++seg) {
             const float* vsrc = A.mode == 1 ? A.vel + (size_t)s * natom * 3
                                             : A.vinit + ((size_t)s * A.nseg + seg) * natom * 3;
@@ -506,16 +738,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                     const int a = b * NT + t;
                     float4 p = sm.pos[a];
                     if (step > 0 && (mobile >> b & 1u)) {  // fix nve/limit: initial_integrate
-                        const float4 fo = sm.frc[a];
-                        v[b][0] += dtf * fo.x;
-                        v[b][1] += dtf * fo.y;
-                        v[b][2] += dtf * fo.z;
-                        const float vsq = v[b][0] * v[b][0] + v[b][1] * v[b][1] + v[b][2] * v[b][2];
-                        if (vsq > vlimsq) {
-                            const float sc = vlim * __frsqrt_rn(vsq);
-#pragma unroll
-                            for (int d = 0; d < 3; ++d) v[b][d] *= sc;
-                        }
+                        kick_limit(v[b][0], v[b][1], v[b][2], f[b][0], f[b][1], f[b][2], dtf, vlim, vlimsq);
                         p.x += dtv * v[b][0];
                         p.y += dtv * v[b][1];
                         p.z += dtv * v[b][2];
@@ -527,7 +750,9 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                     }
                 }
                 if (__syncthreads_or(moved)) {  // neigh_modify every 1 check yes
-                    build_nlist<float, NT, BPT>(natom, sm, nbr, A.cm.kcap, A.P.cut_list, A.cm.error);
+                    const unsigned long long c0 = A.prof ? clock64() : 0;
+                    build_nlist<float, NT, uint16_t>(natom, sm.pos, sm.L, A.P.cut_list, sm.r);
+                    if (A.prof) c_build += clock64() - c0;
                     ++nbuild;
 #pragma unroll
                     for (int b = 0; b < BPT; ++b) {
@@ -537,19 +762,35 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                         xb[b][2] = p.z;
                     }
                 }
-                // forces: the owner thread gathers every contribution of its atoms
+                // forces: the owner thread gathers every contribution of its atoms (one
+                // copy of the force code; per-atom registers picked by conditional moves)
+                const unsigned long long cf0 = A.prof ? clock64() : 0;
+#pragma unroll 1
                 for (int b = 0; b < BPT; ++b) {
                     const int a = b * NT + t;
-                    if (a >= natom) break;
-                    double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
-                    float fx, fy, fz;
-                    atom_force<float, false>(a, sm.pos[a], A.cm.aflags[a], sm.pos,
-                                             nbr + (size_t)(a >> 6) * A.cm.kcap * 64 + lane, sm.nnb[a],
-                                             adj + soff[a >> 6] + lane, deg[a], A.P,
-                                             CellGrid{sm.cell, sm.sorted, sm.cellid, sm.misc + 4}, evf, envf, fx,
-                                             fy, fz, ep, eb,
-                                             ee);
-                    sm.frc[a] = make_float4(fx, fy, fz, 0.f);
+                    if (a < natom) {
+                        double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
+                        float fx, fy, fz;
+                        const BondView B = lds_bonds ? BondView{nullptr, nullptr, sm.rest + sm.boff[a], sm.btab,
+                                                                (int)sm.boff[a + 1] - (int)sm.boff[a]}
+                                                     : BondView{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
+                        atom_force<float, false, uint16_t>(a, sm.pos[a], A.cm.aflags[a], sm.pos, sm.L,
+                                                           pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
+                                                           pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz, ep,
+                                                           eb, ee);
+#pragma unroll
+                        for (int i = 0; i < BPT; ++i)
+                            if (b == i) {
+                                f[i][0] = fx;
+                                f[i][1] = fy;
+                                f[i][2] = fz;
+                            }
+                    }
+                }
+                if (A.prof) {
+                    __syncthreads();  // profiling only: the force phase of every wave
+                    c_force += clock64() - cf0;
+                    ++nstep_total;
                 }
                 if (step == 0) {
                     __syncthreads();  // setup forces read sm.pos: no update before every wave is done
@@ -559,34 +800,17 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
 #pragma unroll
                 for (int b = 0; b < BPT; ++b) {  // final_integrate
                     if (!(mobile >> b & 1u)) continue;
-                    const float4 fo = sm.frc[b * NT + t];
-                    v[b][0] += dtf * fo.x;
-                    v[b][1] += dtf * fo.y;
-                    v[b][2] += dtf * fo.z;
-                    const float vsq = v[b][0] * v[b][0] + v[b][1] * v[b][1] + v[b][2] * v[b][2];
-                    if (vsq > vlimsq) {
-                        const float sc = vlim * __frsqrt_rn(vsq);
-#pragma unroll
-                        for (int d = 0; d < 3; ++d) v[b][d] *= sc;
-                    }
+                    kick_limit(v[b][0], v[b][1], v[b][2], f[b][0], f[b][1], f[b][2], dtf, vlim, vlimsq);
 #pragma unroll
                     for (int d = 0; d < 3; ++d) ts[0] += (double)(v[b][d] * v[b][d]);
                 }
-                block_sum<NT, 1>(ts, (step & 1) ? sm.red1 : sm.red0);
-                // fix temp/rescale 1 t0 t1 window fraction: end_of_step
-                const double tcur = dof > 0 ? ts[0] / dof : 0.0;
-                if (tcur > 0.0) {
-                    const double delta = (double)step / (double)nsteps;
-                    double tt = (double)t0 + delta * ((double)t1 - (double)t0);
-                    if (fabs(tcur - tt) > (double)A.t_window) {
-                        tt = tcur - (double)A.t_fraction * (tcur - tt);
-                        const float factor = (float)sqrt(tt / tcur);
+                block_sum<NT, 1>(ts, (step & 1) ? sm.r.red1 : sm.r.red0);
+                const float factor = temp_rescale_factor(ts[0], dof, step, nsteps, t0, t1, A.t_window, A.t_fraction);
+                if (factor != 1.0f)
 #pragma unroll
-                        for (int b = 0; b < BPT; ++b)
+                    for (int b = 0; b < BPT; ++b)
 #pragma unroll
-                            for (int d = 0; d < 3; ++d) v[b][d] *= factor;
-                    }
-                }
+                        for (int d = 0; d < 3; ++d) v[b][d] *= factor;
             }
         }
         __syncthreads();
@@ -597,7 +821,6 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
             const int a = b * NT + t;
             if (a >= natom) continue;
             const float4 p = sm.pos[a];
-            const float4 fo = sm.frc[a];
             xo[(size_t)a * 3] = p.x;
             xo[(size_t)a * 3 + 1] = p.y;
             xo[(size_t)a * 3 + 2] = p.z;
@@ -605,9 +828,166 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
             for (int d = 0; d < 3; ++d) vo[(size_t)a * 3 + d] = v[b][d];
             if (A.forces_out) {
                 float* fo3 = A.forces_out + ((size_t)s * natom + a) * 3;
-                fo3[0] = fo.x;
-                fo3[1] = fo.y;
-                fo3[2] = fo.z;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) fo3[d] = f[b][d];
+            }
+        }
+        if (t == 0 && A.nrebuild) A.nrebuild[s] = nbuild;
+        if (t == 0 && A.prof) {
+            c_all = clock64() - c_begin;
+            atomicAdd(&A.prof[0], c_build);
+            atomicAdd(&A.prof[1], c_force);
+            atomicAdd(&A.prof[2], c_all - c_build - c_force);
+            atomicAdd(&A.prof[3], nstep_total);
+            atomicAdd(&A.prof[4], (unsigned long long)nbuild);
+        }
+        __syncthreads();
+    }
+}
+
+// The same protocol for structures too large for LDS: positions, Verlet list,
+// cell grid and per-atom v/f/last-build positions in the workgroup's HBM
+// workspace (SoA, coalesced); atoms a = t, t+NT, ...  The temperature rescale
+// factor is applied lazily when a velocity is next read.
+template <int NT>
+__global__ void __launch_bounds__(NT) anneal_big_kernel(AnnealArgs A) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[4096];
+    Carver cv(smem);
+    float* gp;
+    int* gn;
+    const Red R = carve_red<float>(cv, &gp, &gn);
+    const int t = threadIdx.x, lane = t & 63;
+    const int natom = A.cm.natom, ldn = A.cm.ldn;
+    NList<float, int> L;
+    BigWs<float> W;
+    carve_ws<float>(A.ws + (size_t)blockIdx.x * A.ws_stride, natom, ldn, A.cm.kcap, kCellCapBig, true, true, &L, &W);
+    L.gp = gp;
+    L.gn = gn;
+    float4* pos = W.pos;
+    float *V = W.v, *F = W.f, *XB = W.xb;
+    for (;;) {
+        const int s = next_structure(A.cm, R.misc);
+        if (s >= A.cm.nstruct) break;
+        const float* xs = A.xyz + (size_t)s * natom * 3;
+        int nmob = 0;
+        for (int a = t; a < natom; a += NT) {
+            const uint32_t fl = A.cm.aflags[a];
+            nmob += (fl & IGM_ATOM_FIXED) ? 0 : 1;
+            const float r = A.cm.radii[a];
+            pos[a] = make_float4(xs[(size_t)a * 3], xs[(size_t)a * 3 + 1], xs[(size_t)a * 3 + 2],
+                                 (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                V[d * ldn + a] = 0.0f;
+                F[d * ldn + a] = 0.0f;
+                XB[d * ldn + a] = __int_as_float(0x7f800000);
+            }
+        }
+        double cnt[1] = {(double)nmob};
+        block_sum<NT, 1>(cnt, R.red0);
+        const double dof = 3.0 * cnt[0] - 3.0;
+        __syncthreads();
+        const uint32_t* adj = A.cm.bonds.ent + A.cm.bonds.base[s];
+        const int* soff = A.cm.bonds.soff + (size_t)s * (A.cm.nslice + 1);
+        const int* deg = A.cm.bonds.deg + (size_t)s * natom;
+        const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
+        int nbuild = 0;
+        float pending = 1.0f;  // temp/rescale factor not yet applied to V
+        for (int seg = 0; seg < A.nseg; ++seg) {
+            const float* vsrc = A.mode == 1 ? A.vel + (size_t)s * natom * 3
+                                            : A.vinit + ((size_t)s * A.nseg + seg) * natom * 3;
+            for (int a = t; a < natom; a += NT) {
+                const bool mob = !(A.cm.aflags[a] & IGM_ATOM_FIXED);
+#pragma unroll
+                for (int d = 0; d < 3; ++d) V[d * ldn + a] = mob ? vsrc[(size_t)a * 3 + d] : 0.0f;
+            }
+            pending = 1.0f;
+            const int nsteps = A.seg_steps[seg];
+            const float evf = A.seg_evf[seg], envf = A.seg_envf[seg];
+            const float t0 = A.seg_t0[seg], t1 = A.seg_t1[seg];
+            const float dtv = A.dt, dtf = 0.5f * A.dt;
+            const float vlim = A.seg_xmax[seg] / dtv;
+            const float vlimsq = vlim * vlim;
+            const float trig = 0.25f * A.P.skin * A.P.skin;
+            for (int step = 0; step <= nsteps; ++step) {
+                int moved = 0;
+                for (int a = t; a < natom; a += NT) {
+                    float4 p = pos[a];
+                    if (step > 0 && !(A.cm.aflags[a] & IGM_ATOM_FIXED)) {
+                        float vx = V[a] * pending, vy = V[ldn + a] * pending, vz = V[2 * ldn + a] * pending;
+                        kick_limit(vx, vy, vz, F[a], F[ldn + a], F[2 * ldn + a], dtf, vlim, vlimsq);
+                        V[a] = vx;
+                        V[ldn + a] = vy;
+                        V[2 * ldn + a] = vz;
+                        p.x += dtv * vx;
+                        p.y += dtv * vy;
+                        p.z += dtv * vz;
+                        pos[a] = p;
+                    }
+                    if (p.w >= 0.0f) {
+                        const float ddx = p.x - XB[a], ddy = p.y - XB[ldn + a], ddz = p.z - XB[2 * ldn + a];
+                        moved |= !(ddx * ddx + ddy * ddy + ddz * ddz <= trig);
+                    }
+                }
+                pending = 1.0f;
+                if (__syncthreads_or(moved)) {
+                    build_nlist<float, NT, int>(natom, pos, L, A.P.cut_list, R);
+                    ++nbuild;
+                    for (int a = t; a < natom; a += NT) {
+                        const float4 p = pos[a];
+                        XB[a] = p.x;
+                        XB[ldn + a] = p.y;
+                        XB[2 * ldn + a] = p.z;
+                    }
+                }
+                for (int a = t; a < natom; a += NT) {
+                    double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
+                    float fx, fy, fz;
+                    const BondView B{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
+                    atom_force<float, false, int>(a, pos[a], A.cm.aflags[a], pos, L, XB[a], XB[ldn + a],
+                                                  XB[2 * ldn + a], B, A.P, evf, envf, fx, fy, fz, ep, eb, ee);
+                    F[a] = fx;
+                    F[ldn + a] = fy;
+                    F[2 * ldn + a] = fz;
+                }
+                if (step == 0) {
+                    __syncthreads();
+                    continue;
+                }
+                double ts[1] = {0.0};
+                for (int a = t; a < natom; a += NT) {
+                    if (A.cm.aflags[a] & IGM_ATOM_FIXED) continue;
+                    float vx = V[a], vy = V[ldn + a], vz = V[2 * ldn + a];
+                    kick_limit(vx, vy, vz, F[a], F[ldn + a], F[2 * ldn + a], dtf, vlim, vlimsq);
+                    V[a] = vx;
+                    V[ldn + a] = vy;
+                    V[2 * ldn + a] = vz;
+                    ts[0] += (double)(vx * vx) + (double)(vy * vy) + (double)(vz * vz);
+                }
+                block_sum<NT, 1>(ts, (step & 1) ? R.red1 : R.red0);
+                pending = temp_rescale_factor(ts[0], dof, step, nsteps, t0, t1, A.t_window, A.t_fraction);
+            }
+            if (pending != 1.0f) {
+                for (int a = t; a < natom; a += NT)
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) V[d * ldn + a] *= pending;
+                pending = 1.0f;
+            }
+        }
+        __syncthreads();
+        float* xo = A.xyz + (size_t)s * natom * 3;
+        float* vo = A.vel + (size_t)s * natom * 3;
+        for (int a = t; a < natom; a += NT) {
+            const float4 p = pos[a];
+            xo[(size_t)a * 3] = p.x;
+            xo[(size_t)a * 3 + 1] = p.y;
+            xo[(size_t)a * 3 + 2] = p.z;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) vo[(size_t)a * 3 + d] = V[d * ldn + a];
+            if (A.forces_out) {
+                float* fo3 = A.forces_out + ((size_t)s * natom + a) * 3;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) fo3[d] = F[d * ldn + a];
             }
         }
         if (t == 0 && A.nrebuild) A.nrebuild[s] = nbuild;
@@ -670,9 +1050,9 @@ struct CGArgs {
     DevParams P;
     float* xyz;          // (B, natom, 3) in/out
     const float* vel;    // (B, natom, 3) velocities after MD (thermo Temp), may be null
-    uint16_t* nbr_ws;
-    size_t nbr_stride;
-    double* vec_ws;      // per resident workgroup: F, X0, G, H as [4][3][npad] doubles
+    unsigned char* ws;   // per resident workgroup: neighbour structure (+ positions on the HBM path)
+    size_t ws_stride;
+    double* vec_ws;      // per resident workgroup: F, X0, G, H, XB as [5][3][ldn] doubles
     size_t vec_stride;
     igm_opt_info* info;  // (B)
     const int* nrebuild_md;
@@ -687,47 +1067,78 @@ enum { MAXITER = 1, MAXEVAL, ETOL, FTOL, DOWNHILL, ZEROALPHA, ZEROFORCE, ZEROQUA
 // phases of the flattened MinCG::iterate + MinLineSearch::linemin_quadratic
 enum { PH_SETUP, PH_BT, PH_QUAD, PH_RET_ZEROQUAD, PH_RET_ZEROALPHA };
 
-template <int NT, int BPT>
+// LDS layout of the CG kernel: f64 positions + the cell grid / list index in LDS
+// on the LDS path; only the reduction block on the HBM path.
+struct CgLds {
+    Red r;
+    double4* pos;
+    int* cell;
+    uint16_t* nnb;
+    uint16_t* sorted;
+    double* gp;
+    int* gn;
+};
+
+__host__ __device__ inline size_t carve_cg_lds(void* smem, int npad, bool big, CgLds* m) {
+    Carver cv(smem);
+    m->r = carve_red<double>(cv, &m->gp, &m->gn);
+    if (!big) {
+        m->pos = cv.take<double4>(npad);
+        m->cell = cv.take<int>(kCellCap + 8);
+        m->nnb = cv.take<uint16_t>(npad);
+        m->sorted = cv.take<uint16_t>(npad);
+    }
+    return cv.o;
+}
+
+template <int NT, bool BIG>
 __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int npad = NT * BPT;
-    Smem<double> sm = carve<double>(smem, npad);
     const int t = threadIdx.x, lane = t & 63;
-    const int natom = A.cm.natom;
-    uint16_t* nbr = A.nbr_ws + (size_t)blockIdx.x * A.nbr_stride;
+    const int natom = A.cm.natom, ldn = A.cm.ldn;
+    CgLds sm;
+    carve_cg_lds(smem, ldn, BIG, &sm);
+    NList<double, int> L;
+    BigWs<double> W;
+    carve_ws<double>(A.ws + (size_t)blockIdx.x * A.ws_stride, natom, ldn, A.cm.kcap,
+                     BIG ? kCellCapBig : kCellCap, BIG, false, &L, &W);
+    L.gp = sm.gp;
+    L.gn = sm.gn;
+    double4* pos = W.pos;
+    if (!BIG) {
+        pos = sm.pos;
+        L.cell = sm.cell;
+        L.nnb = sm.nnb;
+        L.sorted = sm.sorted;
+    }
+    const Red R = sm.r;
     double* F = A.vec_ws + (size_t)blockIdx.x * A.vec_stride;
-    double* X0 = F + 3 * (size_t)npad;
-    double* G = X0 + 3 * (size_t)npad;
-    double* H = G + 3 * (size_t)npad;
-    double xb[BPT][3];
+    double* X0 = F + 3 * (size_t)ldn;
+    double* G = X0 + 3 * (size_t)ldn;
+    double* H = G + 3 * (size_t)ldn;
+    double* XB = H + 3 * (size_t)ldn;
     const double ALPHA_MAX = 1.0, ALPHA_REDUCE = 0.5, BACKTRACK_SLOPE = 0.4, QUADRATIC_TOL = 0.1, EMACH = 1.0e-8,
                  EPS_QUAD = 1.0e-28;
     for (;;) {
-        if (t == 0) sm.misc[0] = atomicAdd(A.cm.work_counter, 1);
-        __syncthreads();
-        const int s = sm.misc[0];
-        __syncthreads();
+        const int s = next_structure(A.cm, R.misc);
         if (s >= A.cm.nstruct) break;
         const float* xs = A.xyz + (size_t)s * natom * 3;
-#pragma unroll
-        for (int b = 0; b < BPT; ++b) {
-            const int a = b * NT + t;
-            const bool in = a < natom;
-            const uint32_t fl = in ? A.cm.aflags[a] : 0u;
-            const double r = in ? (double)A.cm.atype[a] : 0.0;
-            sm.pos[a] = make_double4(in ? (double)xs[(size_t)a * 3] : 0.0, in ? (double)xs[(size_t)a * 3 + 1] : 0.0,
-                                     in ? (double)xs[(size_t)a * 3 + 2] : 0.0,
-                                     (in && (fl & IGM_ATOM_BEAD)) ? r : -(r + 1.0));
+        for (int a = t; a < natom; a += NT) {
+            const uint32_t fl = A.cm.aflags[a];
+            const double r = (double)A.cm.atype[a];
+            pos[a] = make_double4((double)xs[(size_t)a * 3], (double)xs[(size_t)a * 3 + 1],
+                                  (double)xs[(size_t)a * 3 + 2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0));
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
-                xb[b][d] = __longlong_as_double(0x7ff0000000000000LL);
-                F[d * npad + a] = 0.0;
+                XB[d * ldn + a] = __longlong_as_double(0x7ff0000000000000LL);
+                F[d * ldn + a] = 0.0;
             }
         }
         __syncthreads();
-        const int4* adj = A.cm.bonds.ent + A.cm.bonds.base[s];
+        const uint32_t* adj = A.cm.bonds.ent + A.cm.bonds.base[s];
         const int* soff = A.cm.bonds.soff + (size_t)s * (A.cm.nslice + 1);
         const int* deg = A.cm.bonds.deg + (size_t)s * natom;
+        const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
         const double trig = 0.25 * (double)A.P.skin * (double)A.P.skin;
         int neval = 0, nbuild = 0, niter = 0, stop = MAXITER;
         double ecurrent = 0, einitial = 0, eoriginal = 0, eprevious = 0;
@@ -738,53 +1149,45 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
         for (;;) {
             // ---------- the single energy/force evaluation site
             int moved = 0;
-#pragma unroll
-            for (int b = 0; b < BPT; ++b) {
-                const int a = b * NT + t;
-                double4 p = sm.pos[a];
-                if (a_eval >= 0.0 && a < natom) {  // alpha_step: x = x0 + alpha h
+            for (int a = t; a < natom; a += NT) {
+                double4 p = pos[a];
+                if (a_eval >= 0.0) {  // alpha_step: x = x0 + alpha h
                     p.x = X0[a] + (a_eval > 0.0 ? a_eval * H[a] : 0.0);
-                    p.y = X0[npad + a] + (a_eval > 0.0 ? a_eval * H[npad + a] : 0.0);
-                    p.z = X0[2 * npad + a] + (a_eval > 0.0 ? a_eval * H[2 * npad + a] : 0.0);
-                    sm.pos[a] = p;
+                    p.y = X0[ldn + a] + (a_eval > 0.0 ? a_eval * H[ldn + a] : 0.0);
+                    p.z = X0[2 * ldn + a] + (a_eval > 0.0 ? a_eval * H[2 * ldn + a] : 0.0);
+                    pos[a] = p;
                 }
                 if (p.w >= 0.0) {
-                    const double dx = p.x - xb[b][0], dy = p.y - xb[b][1], dz = p.z - xb[b][2];
+                    const double dx = p.x - XB[a], dy = p.y - XB[ldn + a], dz = p.z - XB[2 * ldn + a];
                     moved |= !(dx * dx + dy * dy + dz * dz <= trig);
                 }
             }
             if (a_eval >= 0.0) ++neval;
             if (__syncthreads_or(moved)) {
-                build_nlist<double, NT, BPT>(natom, sm, nbr, A.cm.kcap, (double)A.P.cut_list, A.cm.error);
+                build_nlist<double, NT, int>(natom, pos, L, (double)A.P.cut_list, R);
                 ++nbuild;
-#pragma unroll
-                for (int b = 0; b < BPT; ++b) {
-                    const double4 p = sm.pos[b * NT + t];
-                    xb[b][0] = p.x;
-                    xb[b][1] = p.y;
-                    xb[b][2] = p.z;
+                for (int a = t; a < natom; a += NT) {
+                    const double4 p = pos[a];
+                    XB[a] = p.x;
+                    XB[ldn + a] = p.y;
+                    XB[2 * ldn + a] = p.z;
                 }
             }
             double vv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int b = 0; b < BPT; ++b) {
-                const int a = b * NT + t;
-                if (a >= natom) break;
+            for (int a = t; a < natom; a += NT) {
                 double e_e[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
                 double fx, fy, fz;
-                atom_force<double, true>(a, sm.pos[a], A.cm.aflags[a], sm.pos,
-                                         nbr + (size_t)(a >> 6) * A.cm.kcap * 64 + lane, sm.nnb[a],
-                                         adj + soff[a >> 6] + lane, deg[a], A.P,
-                                         CellGrid{sm.cell, sm.sorted, sm.cellid, sm.misc + 4}, A.evf, A.envf, fx,
-                                         fy, fz, vv[0],
-                                         vv[1], e_e);
+                const BondView B{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
+                atom_force<double, true, int>(a, pos[a], A.cm.aflags[a], pos, L, XB[a], XB[ldn + a],
+                                              XB[2 * ldn + a], B, A.P, A.evf, A.envf, fx, fy, fz, vv[0], vv[1], e_e);
                 for (int e = 0; e < IGM_MAX_ENVELOPES; ++e) vv[2 + e] += e_e[e];
                 F[a] = fx;
-                F[npad + a] = fy;
-                F[2 * npad + a] = fz;
+                F[ldn + a] = fy;
+                F[2 * ldn + a] = fz;
                 vv[6] += fx * fx + fy * fy + fz * fz;
-                if (phase != PH_SETUP) vv[7] += fx * H[a] + fy * H[npad + a] + fz * H[2 * npad + a];
+                if (phase != PH_SETUP) vv[7] += fx * H[a] + fy * H[ldn + a] + fz * H[2 * ldn + a];
             }
-            block_sum<NT, 8>(vv, sm.red0);
+            block_sum<NT, 8>(vv, R.red0);
             __syncthreads();
             ep = vv[0];
             eb = vv[1];
@@ -798,12 +1201,9 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
             if (phase == PH_SETUP) {  // Min::setup, then the MinCG::iterate prologue
                 einitial = ecurrent;
                 if (A.mode == 1) break;
-                for (int b = 0; b < BPT; ++b) {
-                    const int a = b * NT + t;
-                    if (a >= natom) break;
+                for (int a = t; a < natom; a += NT)
 #pragma unroll
-                    for (int d = 0; d < 3; ++d) G[d * npad + a] = H[d * npad + a] = F[d * npad + a];
-                }
+                    for (int d = 0; d < 3; ++d) G[d * ldn + a] = H[d * ldn + a] = F[d * ldn + a];
                 ggv = ff;
                 start_iter = true;
             } else if (phase == PH_RET_ZEROQUAD) {
@@ -871,39 +1271,30 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
                     break;
                 }
                 double dd[1] = {0.0};
-                for (int b = 0; b < BPT; ++b) {
-                    const int a = b * NT + t;
-                    if (a >= natom) break;
+                for (int a = t; a < natom; a += NT)
 #pragma unroll
-                    for (int d = 0; d < 3; ++d) dd[0] += F[d * npad + a] * G[d * npad + a];
-                }
-                block_sum<NT, 1>(dd, sm.red1);
+                    for (int d = 0; d < 3; ++d) dd[0] += F[d * ldn + a] * G[d * ldn + a];
+                block_sum<NT, 1>(dd, R.red1);
                 __syncthreads();
                 double beta = fmax(0.0, (ff - dd[0]) / ggv);
                 if ((long)(niter + 1) % (3L * natom) == 0) beta = 0.0;
                 ggv = ff;
                 double gh[1] = {0.0};
-                for (int b = 0; b < BPT; ++b) {
-                    const int a = b * NT + t;
-                    if (a >= natom) break;
+                for (int a = t; a < natom; a += NT)
 #pragma unroll
                     for (int d = 0; d < 3; ++d) {
-                        const double fv = F[d * npad + a];
-                        const double hv = fv + beta * H[d * npad + a];
-                        G[d * npad + a] = fv;
-                        H[d * npad + a] = hv;
+                        const double fv = F[d * ldn + a];
+                        const double hv = fv + beta * H[d * ldn + a];
+                        G[d * ldn + a] = fv;
+                        H[d * ldn + a] = hv;
                         gh[0] += fv * hv;
                     }
-                }
-                block_sum<NT, 1>(gh, sm.red1);
+                block_sum<NT, 1>(gh, R.red1);
                 __syncthreads();
                 if (gh[0] <= 0.0)
-                    for (int b = 0; b < BPT; ++b) {
-                        const int a = b * NT + t;
-                        if (a >= natom) break;
+                    for (int a = t; a < natom; a += NT)
 #pragma unroll
-                        for (int d = 0; d < 3; ++d) H[d * npad + a] = G[d * npad + a];
-                    }
+                        for (int d = 0; d < 3; ++d) H[d * ldn + a] = G[d * ldn + a];
                 start_iter = true;
             }
             if (!start_iter) break;  // unreachable
@@ -916,23 +1307,21 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
             eprevious = ecurrent;
             eoriginal = ecurrent;
             double pr[1] = {0.0}, hm[1] = {0.0};
-            for (int b = 0; b < BPT; ++b) {
-                const int a = b * NT + t;
-                if (a >= natom) break;
-                const double4 p = sm.pos[a];
+            for (int a = t; a < natom; a += NT) {
+                const double4 p = pos[a];
                 X0[a] = p.x;
-                X0[npad + a] = p.y;
-                X0[2 * npad + a] = p.z;
+                X0[ldn + a] = p.y;
+                X0[2 * ldn + a] = p.z;
 #pragma unroll
                 for (int d = 0; d < 3; ++d) {
-                    const double hv = H[d * npad + a];
-                    pr[0] += F[d * npad + a] * hv;
+                    const double hv = H[d * ldn + a];
+                    pr[0] += F[d * ldn + a] * hv;
                     hm[0] = fmax(hm[0], fabs(hv));
                 }
             }
-            block_sum<NT, 1>(pr, sm.red1);
+            block_sum<NT, 1>(pr, R.red1);
             __syncthreads();
-            block_max<NT, 1>(hm, sm.red0);
+            block_max<NT, 1>(hm, R.red0);
             __syncthreads();
             fdothall = pr[0];
             if (fdothall <= 0.0) {
@@ -953,23 +1342,19 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
         }
         // ---------- outputs
         double fn[2] = {0.0, 0.0};
-        for (int b = 0; b < BPT; ++b) {
-            const int a = b * NT + t;
-            if (a >= natom) break;
+        for (int a = t; a < natom; a += NT) {
 #pragma unroll
-            for (int d = 0; d < 3; ++d) fn[0] += F[d * npad + a] * F[d * npad + a];
+            for (int d = 0; d < 3; ++d) fn[0] += F[d * ldn + a] * F[d * ldn + a];
             if (A.vel) {
                 const float* vs = A.vel + ((size_t)s * natom + a) * 3;
 #pragma unroll
                 for (int d = 0; d < 3; ++d) fn[1] += (double)vs[d] * (double)vs[d];
             }
         }
-        block_sum<NT, 2>(fn, sm.red1);
+        block_sum<NT, 2>(fn, R.red1);
         float* xo = A.xyz + (size_t)s * natom * 3;
-        for (int b = 0; b < BPT; ++b) {
-            const int a = b * NT + t;
-            if (a >= natom) break;
-            const double4 p = sm.pos[a];
+        for (int a = t; a < natom; a += NT) {
+            const double4 p = pos[a];
             if (A.mode == 0) {
                 xo[(size_t)a * 3] = (float)p.x;
                 xo[(size_t)a * 3 + 1] = (float)p.y;
@@ -977,7 +1362,7 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
             }
             if (A.forces_out)
 #pragma unroll
-                for (int d = 0; d < 3; ++d) A.forces_out[((size_t)s * natom + a) * 3 + d] = (float)F[d * npad + a];
+                for (int d = 0; d < 3; ++d) A.forces_out[((size_t)s * natom + a) * 3 + d] = (float)F[d * ldn + a];
         }
         if (t == 0) {
             if (A.info) {
@@ -1009,96 +1394,181 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
 }
 
 // ------------------------------------------------------------- adjacency
+// Per structure: degrees, bond types (distinct (r0, k), sorted by their bit
+// pattern -> deterministic ids) and the compact sliced-ELLPACK entries.
 __device__ __forceinline__ const igm_bond& bond_at(const igm_bond* shared, int64_t nshared, const igm_bond* own,
                                                    int64_t q) {
     return q < nshared ? shared[q] : own[q - nshared];
 }
 
-__global__ void adj_count_kernel(int nstruct, int natom, int nslice, const igm_bond* shared, int64_t nshared,
-                                 const int64_t* sptr, const igm_bond* sbonds, int* deg, int* soff, int64_t* size,
-                                 int* error) {
-    extern __shared__ int cnt[];
-    const int s = blockIdx.x;
+__device__ __forceinline__ uint64_t bond_key(const igm_bond& b) {
+    return ((uint64_t)__float_as_uint(b.r0) << 32) | (uint64_t)__float_as_uint(b.k);
+}
+
+__device__ __forceinline__ uint32_t key_hash(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    return (uint32_t)k & (kTypeHash - 1);
+}
+
+constexpr uint64_t kEmptyKey = ~0ull;
+
+// insert every bond key of structure s into the LDS hash; returns (uniform) the
+// number of distinct keys, or > kMaxBondTypes if the structure has too many
+__device__ int hash_bond_types(uint64_t* hash, const igm_bond* shared, int64_t nshared, const igm_bond* own,
+                               int64_t nb, int* nuniq) {
     const int t = threadIdx.x;
-    for (int a = t; a < nslice * 64; a += blockDim.x) cnt[a] = 0;
+    for (int i = t; i < kTypeHash; i += blockDim.x) hash[i] = kEmptyKey;
+    if (t == 0) *nuniq = 0;
     __syncthreads();
+    for (int64_t q = t; q < nb; q += blockDim.x) {
+        const uint64_t key = bond_key(bond_at(shared, nshared, own, q));
+        uint32_t h = key_hash(key);
+        for (int probe = 0; probe < kTypeHash; ++probe) {
+            const uint64_t prev = atomicCAS((unsigned long long*)&hash[h], (unsigned long long)kEmptyKey,
+                                            (unsigned long long)key);
+            if (prev == kEmptyKey) {
+                atomicAdd(nuniq, 1);
+                break;
+            }
+            if (prev == key) break;
+            h = (h + 1) & (kTypeHash - 1);
+        }
+    }
+    __syncthreads();
+    const int n = *nuniq;
+    __syncthreads();
+    return n;
+}
+
+__global__ void adj_degree_kernel(int natom, const igm_bond* shared, int64_t nshared, const int64_t* sptr,
+                                  const igm_bond* sbonds, int* deg, int64_t* ntype, int* error) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_adj[];
+    uint64_t* hash = reinterpret_cast<uint64_t*>(smem_adj);
+    int* nuniq = reinterpret_cast<int*>(hash + kTypeHash);
+    const int s = blockIdx.x;
     const int64_t b0 = sptr ? sptr[s] : 0, b1 = sptr ? sptr[s + 1] : 0;
     const igm_bond* own = sbonds ? sbonds + b0 : nullptr;
     const int64_t nb = nshared + (b1 - b0);
-    for (int64_t q = t; q < nb; q += blockDim.x) {
+    int* dg = deg + (size_t)s * natom;
+    for (int64_t q = threadIdx.x; q < nb; q += blockDim.x) {
         const igm_bond& bd = bond_at(shared, nshared, own, q);
         const uint32_t i = bd.i, j = bd.j & 0x7fffffffu;
         if (i >= (uint32_t)natom || j >= (uint32_t)natom) {
             atomicOr(error, 2);
             continue;
         }
-        atomicAdd(&cnt[i], 1);
-        atomicAdd(&cnt[j], 1);
+        atomicAdd(&dg[i], 1);
+        atomicAdd(&dg[j], 1);
     }
-    __syncthreads();
-    for (int a = t; a < natom; a += blockDim.x) deg[(size_t)s * natom + a] = cnt[a];
-    __syncthreads();
-    // per-slice max degree (thread per slice), stored back into cnt[slice*64]
-    for (int sl = t; sl < nslice; sl += blockDim.x) {
-        int m = 0;
-        for (int l = 0; l < 64; ++l) m = max(m, cnt[sl * 64 + l]);
-        cnt[sl * 64] = m;
-    }
-    __syncthreads();
-    if (t == 0) {
-        int acc = 0;
-        int* so = soff + (size_t)s * (nslice + 1);
-        for (int sl = 0; sl < nslice; ++sl) {
-            so[sl] = acc;
-            acc += cnt[sl * 64] * 64;
-        }
-        so[nslice] = acc;
-        size[s] = acc;
+    const int n = hash_bond_types(hash, shared, nshared, own, nb, nuniq);
+    if (threadIdx.x == 0) {
+        ntype[s] = n;
+        if (n > kMaxBondTypes) atomicOr(error, 4);
     }
 }
 
-__global__ void adj_fill_kernel(int nstruct, int natom, int nslice, const igm_bond* shared, int64_t nshared,
-                                const int64_t* sptr, const igm_bond* sbonds, const int* deg, const int* soff,
-                                const int64_t* base, int4* ent) {
-    extern __shared__ int fill[];
+// per-slice max degree -> slice offsets (runs after adj_degree_kernel completed)
+__global__ void adj_slices_kernel(int natom, int nslice, const int* deg, int* soff, int64_t* size) {
+    __shared__ int smax[1024];
+    const int s = blockIdx.x;
+    const int* dg = deg + (size_t)s * natom;
+    for (int sl0 = 0; sl0 < nslice; sl0 += 1024) {
+        const int sl = sl0 + (int)threadIdx.x;
+        __syncthreads();
+        if (threadIdx.x < 1024) {
+            int m = 0;
+            if (sl < nslice)
+                for (int l = 0; l < 64; ++l) {
+                    const int a = sl * 64 + l;
+                    if (a < natom) m = max(m, dg[a]);
+                }
+            smax[threadIdx.x] = m;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t acc = sl0 == 0 ? 0 : (int64_t)soff[(size_t)s * (nslice + 1) + sl0];
+            int* so = soff + (size_t)s * (nslice + 1);
+            for (int i = 0; i < 1024 && sl0 + i < nslice; ++i) {
+                so[sl0 + i] = (int)acc;
+                acc += (int64_t)smax[i] * 64;
+            }
+            so[min(sl0 + 1024, nslice)] = (int)acc;
+            if (sl0 + 1024 >= nslice) size[s] = acc;
+        }
+    }
+}
+
+__global__ void adj_fill_kernel(int natom, int nslice, const igm_bond* shared, int64_t nshared, const int64_t* sptr,
+                                const igm_bond* sbonds, const int* deg, const int* soff, const int64_t* base,
+                                const int64_t* tbase, int* fillc, uint32_t* ent, float2* types) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_adj[];
+    uint64_t* hash = reinterpret_cast<uint64_t*>(smem_adj);
+    int* nuniq = reinterpret_cast<int*>(hash + kTypeHash);
+    uint64_t* uniq = hash + kTypeHash + 2;  // kMaxBondTypes sorted keys
+    __shared__ int ncomp;
     const int s = blockIdx.x;
     const int t = threadIdx.x;
-    for (int a = t; a < natom; a += blockDim.x) fill[a] = 0;
-    __syncthreads();
     const int64_t b0 = sptr ? sptr[s] : 0, b1 = sptr ? sptr[s + 1] : 0;
     const igm_bond* own = sbonds ? sbonds + b0 : nullptr;
     const int64_t nb = nshared + (b1 - b0);
+    const int n = hash_bond_types(hash, shared, nshared, own, nb, nuniq);
+    if (n > kMaxBondTypes) return;  // reported by adj_degree_kernel
+    // compact the keys, then rank them: id = #keys below (deterministic)
+    if (t == 0) ncomp = 0;
+    __syncthreads();
+    for (int i = t; i < kTypeHash; i += blockDim.x)
+        if (hash[i] != kEmptyKey) uniq[atomicAdd(&ncomp, 1)] = hash[i];
+    __syncthreads();
+    float2* tt = types + tbase[s];
+    for (int i = t; i < n; i += blockDim.x) {
+        const uint64_t k = uniq[i];
+        int r = 0;
+        for (int q = 0; q < n; ++q) r += uniq[q] < k ? 1 : 0;
+        hash[r] = k;  // the hash is dead: reuse it as the sorted table
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += blockDim.x) {
+        const uint64_t k = hash[i];
+        tt[i] = make_float2(__uint_as_float((uint32_t)(k >> 32)), __uint_as_float((uint32_t)k));
+    }
     const int* so = soff + (size_t)s * (nslice + 1);
-    int4* E = ent + base[s];
+    uint32_t* E = ent + base[s];
+    int* fc = fillc + (size_t)s * natom;
     for (int64_t q = t; q < nb; q += blockDim.x) {
         const igm_bond& bd = bond_at(shared, nshared, own, q);
         const uint32_t i = bd.i, j = bd.j & 0x7fffffffu, low = bd.j & kLowerBit;
         if (i >= (uint32_t)natom || j >= (uint32_t)natom) continue;
-        const int si = atomicAdd(&fill[i], 1);
-        const int sj = atomicAdd(&fill[j], 1);
-        E[so[i >> 6] + si * 64 + (i & 63)] = make_int4((int)(j | low), __float_as_int(bd.r0), __float_as_int(bd.k), 0);
-        E[so[j >> 6] + sj * 64 + (j & 63)] = make_int4((int)(i | low), __float_as_int(bd.r0), __float_as_int(bd.k), 0);
+        const uint64_t key = bond_key(bd);
+        int lo = 0, hi = n - 1;
+        while (lo < hi) {  // lower_bound in the sorted table
+            const int mid = (lo + hi) >> 1;
+            if (hash[mid] < key)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        const uint32_t tid = (uint32_t)lo << 16;
+        const int si = atomicAdd(&fc[i], 1);
+        const int sj = atomicAdd(&fc[j], 1);
+        E[so[i >> 6] + (size_t)si * 64 + (i & 63)] = j | tid | low;
+        E[so[j >> 6] + (size_t)sj * 64 + (j & 63)] = i | tid | low;
     }
     __syncthreads();
-    __threadfence_block();
-    // fixed order per atom: sort entries by (partner|style, r0, k)
+    // fixed order per atom: sort the entries
+    const int* dg = deg + (size_t)s * natom;
     for (int a = t; a < natom; a += blockDim.x) {
-        const int n = deg[(size_t)s * natom + a];
-        int4* L = E + so[a >> 6] + (a & 63);
-        for (int i = 1; i < n; ++i) {
-            const int4 v = L[(size_t)i * 64];
+        const int m = dg[a];
+        uint32_t* Lp = E + so[a >> 6] + (a & 63);
+        for (int i = 1; i < m; ++i) {
+            const uint32_t v = Lp[(size_t)i * 64];
             int k = i - 1;
-            while (k >= 0) {
-                const int4 u = L[(size_t)k * 64];
-                const bool gt = ((uint32_t)u.x > (uint32_t)v.x) ||
-                                ((uint32_t)u.x == (uint32_t)v.x &&
-                                 ((uint32_t)u.y > (uint32_t)v.y ||
-                                  ((uint32_t)u.y == (uint32_t)v.y && (uint32_t)u.z > (uint32_t)v.z)));
-                if (!gt) break;
-                L[(size_t)(k + 1) * 64] = u;
+            while (k >= 0 && Lp[(size_t)k * 64] > v) {
+                Lp[(size_t)(k + 1) * 64] = Lp[(size_t)k * 64];
                 --k;
             }
-            L[(size_t)(k + 1) * 64] = v;
+            Lp[(size_t)(k + 1) * 64] = v;
         }
     }
 }
@@ -1115,8 +1585,8 @@ namespace {
 struct Prepared {
     Common cm;
     DevParams P;
-    int npad_needed;
     int64_t total_ent;
+    bool big;  // HBM-resident kernels
 };
 
 // The reference writes np.float32 values with Python's shortest round-trip repr
@@ -1154,9 +1624,9 @@ int make_devparams(igm_ctx* c, const igm_mstep_params* prm, int natom, const flo
         P->env_k_d[e] = prm->env_k[e];
     }
     P->skin = prm->skin > 0 ? (float)prm->skin : rmax;  // LAMMPS 'neighbor maxrad bin'
+    if (const char* e = getenv("IGM_SKIN_FACTOR")) P->skin = (float)(atof(e) * rmax);  // tuning only
     P->cut_list = 2.0f * rmax + P->skin;
-    P->kcap = prm->neigh_capacity > 0 ? prm->neigh_capacity : 128;
-    if (P->kcap >= kNnbWalk) return fail(c, IGM_E_INVALID, "neigh_capacity must be < %d", kNnbWalk);
+    P->kcap = prm->neigh_capacity > 0 ? prm->neigh_capacity : kNeighBudget;
     P->natom = natom;
     P->nslice = (natom + 63) / 64;
     // atom types: one per distinct f32 radius, in order of first appearance
@@ -1199,6 +1669,33 @@ int make_devparams(igm_ctx* c, const igm_mstep_params* prm, int natom, const flo
     return IGM_OK;
 }
 
+// LDS path launch configuration: NT threads, BPT atoms per thread
+struct LaunchCfg {
+    int nt, bpt;
+};
+
+// 1024 threads x 3 atoms measured fastest for 2 Mb structures (profiles/); the
+// choice can be overridden with IGM_MD_CFG=<threads>x<atoms per thread> (tuning).
+bool lds_fits(int natom, LaunchCfg* cfg) {
+    static const int opts[][2] = {{256, 1}, {512, 1}, {768, 1}, {1024, 1}, {1024, 2}, {1024, 3},
+                                  {768, 4}, {512, 6}};
+    int want_nt = 0, want_bpt = 0;
+    if (const char* e = getenv("IGM_MD_CFG")) sscanf(e, "%dx%d", &want_nt, &want_bpt);
+    for (auto& o : opts)
+        if (o[0] * o[1] >= natom && (!want_nt || (o[0] == want_nt && o[1] == want_bpt))) {
+            const int npad = o[0] * o[1];
+            const MdLds m = carve_md_lds(nullptr, npad);
+            // the list region doubles as the build's int scratch
+            if ((size_t)kLdsListSlots * npad * 2 < build_scratch_bytes(kCellCap, npad) || m.rest_cap < 0) return false;
+            CgLds cg;
+            if (carve_cg_lds(nullptr, npad, false, &cg) > kLdsBytes) return false;
+            cfg->nt = o[0];
+            cfg->bpt = o[1];
+            return true;
+        }
+    return false;
+}
+
 // stage inputs + build the bond adjacency for all structures
 int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nstruct, int32_t natom,
             const float* radii, const uint32_t* atom_flags, const igm_bond* shared_bonds, int64_t nshared,
@@ -1229,21 +1726,33 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
     const int* d_atype;
     IGM_TRY(make_devparams(c, prm, natom, d_radii, d_flags, &P, &d_atype));
     const int nslice = P.nslice;
-    void *p_deg, *p_soff, *p_size, *p_base, *p_err, *p_wc;
+    void *p_deg, *p_fill, *p_soff, *p_size, *p_base, *p_nt, *p_tb, *p_err, *p_wc;
     IGM_TRY(workspace(c, "ms_deg", sizeof(int) * (size_t)nstruct * natom, &p_deg));
+    IGM_TRY(workspace(c, "ms_fill", sizeof(int) * (size_t)nstruct * natom, &p_fill));
     IGM_TRY(workspace(c, "ms_soff", sizeof(int) * (size_t)nstruct * (nslice + 1), &p_soff));
     IGM_TRY(workspace(c, "ms_size", sizeof(int64_t) * (size_t)nstruct, &p_size));
     IGM_TRY(workspace(c, "ms_base", sizeof(int64_t) * (size_t)nstruct, &p_base));
+    IGM_TRY(workspace(c, "ms_ntype", sizeof(int64_t) * (size_t)nstruct, &p_nt));
+    IGM_TRY(workspace(c, "ms_tbase", sizeof(int64_t) * (size_t)nstruct, &p_tb));
     IGM_TRY(workspace(c, "ms_err", sizeof(int) * 4, &p_err));
     IGM_TRY(workspace(c, "ms_wc", sizeof(int) * 4, &p_wc));
     int* d_err = (int*)p_err;
     IGM_HIP_CHECK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, c->stream));
-    const size_t lds_cnt = sizeof(int) * (size_t)nslice * 64;
-    if (lds_cnt > 160 * 1024) return fail(c, IGM_E_UNSUPPORTED, "natom too large for the adjacency builder");
+    IGM_HIP_CHECK(c, hipMemsetAsync(p_deg, 0, sizeof(int) * (size_t)nstruct * natom, c->stream));
+    IGM_HIP_CHECK(c, hipMemsetAsync(p_fill, 0, sizeof(int) * (size_t)nstruct * natom, c->stream));
+    const size_t lds_deg = sizeof(uint64_t) * kTypeHash + 16;
+    const size_t lds_fill = lds_deg + sizeof(uint64_t) * kMaxBondTypes;
     {
         Timed tm(c, "adjacency");
-        hipLaunchKernelGGL(adj_count_kernel, dim3(nstruct), dim3(256), lds_cnt, c->stream, nstruct, natom, nslice,
-                           d_shared, nshared, d_sptr, d_sb, (int*)p_deg, (int*)p_soff, (int64_t*)p_size, d_err);
+        IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)adj_degree_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_deg));
+        IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)adj_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds_fill));
+        hipLaunchKernelGGL(adj_degree_kernel, dim3(nstruct), dim3(256), lds_deg, c->stream, natom, d_shared, nshared,
+                           d_sptr, d_sb, (int*)p_deg, (int64_t*)p_nt, d_err);
+        IGM_HIP_CHECK(c, hipGetLastError());
+        hipLaunchKernelGGL(adj_slices_kernel, dim3(nstruct), dim3(1024), 0, c->stream, natom, nslice,
+                           (const int*)p_deg, (int*)p_soff, (int64_t*)p_size);
         IGM_HIP_CHECK(c, hipGetLastError());
         size_t tmp_bytes = 0;
         IGM_HIP_CHECK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, (int64_t*)p_size, (int64_t*)p_base,
@@ -1252,57 +1761,58 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
         IGM_TRY(workspace(c, "ms_scan_tmp", tmp_bytes, &d_tmp));
         IGM_HIP_CHECK(c, hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, (int64_t*)p_size, (int64_t*)p_base,
                                                           nstruct, c->stream));
-        int64_t last_base = 0, last_size = 0;
+        IGM_HIP_CHECK(c, hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, (int64_t*)p_nt, (int64_t*)p_tb, nstruct,
+                                                          c->stream));
+        int64_t last[4] = {0, 0, 0, 0};
         int herr = 0;
-        IGM_HIP_CHECK(c, hipMemcpyAsync(&last_base, (int64_t*)p_base + nstruct - 1, sizeof(int64_t),
+        IGM_HIP_CHECK(c, hipMemcpyAsync(&last[0], (int64_t*)p_base + nstruct - 1, sizeof(int64_t),
                                         hipMemcpyDeviceToHost, c->stream));
-        IGM_HIP_CHECK(c, hipMemcpyAsync(&last_size, (int64_t*)p_size + nstruct - 1, sizeof(int64_t),
+        IGM_HIP_CHECK(c, hipMemcpyAsync(&last[1], (int64_t*)p_size + nstruct - 1, sizeof(int64_t),
+                                        hipMemcpyDeviceToHost, c->stream));
+        IGM_HIP_CHECK(c, hipMemcpyAsync(&last[2], (int64_t*)p_tb + nstruct - 1, sizeof(int64_t),
+                                        hipMemcpyDeviceToHost, c->stream));
+        IGM_HIP_CHECK(c, hipMemcpyAsync(&last[3], (int64_t*)p_nt + nstruct - 1, sizeof(int64_t),
                                         hipMemcpyDeviceToHost, c->stream));
         IGM_HIP_CHECK(c, hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
         IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
         if (herr & 2) return fail(c, IGM_E_INVALID, "bond atom index out of range");
-        const int64_t total = last_base + last_size;
-        void* p_ent;
-        IGM_TRY(workspace(c, "ms_ent", sizeof(int4) * (size_t)(total > 0 ? total : 1), &p_ent));
-        const size_t lds_fill = sizeof(int) * (size_t)natom;
-        hipLaunchKernelGGL(adj_fill_kernel, dim3(nstruct), dim3(256), lds_fill, c->stream, nstruct, natom, nslice,
-                           d_shared, nshared, d_sptr, d_sb, (const int*)p_deg, (const int*)p_soff,
-                           (const int64_t*)p_base, (int4*)p_ent);
+        if (herr & 4)
+            return fail(c, IGM_E_UNSUPPORTED, "a structure has more than %d distinct bond (r0, k) types",
+                        kMaxBondTypes);
+        const int64_t total = last[0] + last[1], ntypes = last[2] + last[3];
+        void *p_ent, *p_types;
+        IGM_TRY(workspace(c, "ms_ent", sizeof(uint32_t) * (size_t)(total > 0 ? total : 1), &p_ent));
+        IGM_TRY(workspace(c, "ms_types", sizeof(float2) * (size_t)(ntypes > 0 ? ntypes : 1), &p_types));
+        hipLaunchKernelGGL(adj_fill_kernel, dim3(nstruct), dim3(256), lds_fill, c->stream, natom, nslice, d_shared,
+                           nshared, d_sptr, d_sb, (const int*)p_deg, (const int*)p_soff, (const int64_t*)p_base,
+                           (const int64_t*)p_tb, (int*)p_fill, (uint32_t*)p_ent, (float2*)p_types);
         IGM_HIP_CHECK(c, hipGetLastError());
         out->total_ent = total;
-        out->cm.bonds.ent = (const int4*)p_ent;
+        out->cm.bonds.ent = (const uint32_t*)p_ent;
+        out->cm.bonds.types = (const float2*)p_types;
     }
     out->cm.nstruct = nstruct;
     out->cm.natom = natom;
     out->cm.nslice = nslice;
-    out->cm.kcap = P.kcap;
+    out->cm.ldn = nslice * 64;
     out->cm.radii = d_radii;
     out->cm.atype = d_atype;
     out->cm.aflags = d_flags;
     out->cm.bonds.base = (const int64_t*)p_base;
     out->cm.bonds.soff = (const int*)p_soff;
     out->cm.bonds.deg = (const int*)p_deg;
+    out->cm.bonds.tbase = (const int64_t*)p_tb;
+    out->cm.bonds.ntype = (const int64_t*)p_nt;
     out->cm.work_counter = (int*)p_wc;
     out->cm.error = d_err;
+    // Verlet-list slots per atom; the HBM part must also hold the build's int scratch
+    int kcap = P.kcap;
+    while ((size_t)out->cm.ldn * kcap * 2 < build_scratch_bytes(kCellCapBig, out->cm.ldn)) ++kcap;
+    out->cm.kcap = kcap;
+    LaunchCfg cfg;
+    out->big = (prm->flags & IGM_MSTEP_FORCE_GLOBAL) || !lds_fits(natom, &cfg);
     out->P = P;
     return IGM_OK;
-}
-
-// launch configuration: NT threads, BPT atoms per thread
-struct LaunchCfg {
-    int nt, bpt;
-};
-
-int pick_cfg(igm_ctx* c, int natom, LaunchCfg* cfg) {
-    static const int opts[][2] = {{256, 1}, {512, 1}, {1024, 1}, {1024, 2}, {1024, 3}};
-    for (auto& o : opts)
-        if (o[0] * o[1] >= natom) {
-            cfg->nt = o[0];
-            cfg->bpt = o[1];
-            return IGM_OK;
-        }
-    return fail(c, IGM_E_UNSUPPORTED,
-                "natom=%d exceeds the LDS-resident M-step kernel (max 3072 atoms per structure)", natom);
 }
 
 #define IGM_DISPATCH_CFG(NTV, BPTV, ...)                           \
@@ -1316,8 +1826,11 @@ int pick_cfg(igm_ctx* c, int natom, LaunchCfg* cfg) {
     bool done = false;                                             \
     IGM_DISPATCH_CFG(256, 1, __VA_ARGS__)                          \
     else IGM_DISPATCH_CFG(512, 1, __VA_ARGS__)                     \
+    else IGM_DISPATCH_CFG(768, 1, __VA_ARGS__)                     \
     else IGM_DISPATCH_CFG(1024, 1, __VA_ARGS__)                    \
     else IGM_DISPATCH_CFG(1024, 2, __VA_ARGS__)                    \
+    else IGM_DISPATCH_CFG(768, 4, __VA_ARGS__)                     \
+    else IGM_DISPATCH_CFG(512, 6, __VA_ARGS__)                     \
     else IGM_DISPATCH_CFG(1024, 3, __VA_ARGS__)                    \
     if (!done) return fail(c, IGM_E_UNSUPPORTED, "no kernel configuration");
 
@@ -1331,11 +1844,11 @@ int resident_grid(igm_ctx* c, KernelT kernel, int nt, size_t lds, int nstruct, i
     return IGM_OK;
 }
 
+constexpr int kBigNT = 512;
+
 int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, float* d_xyz, float* d_vel,
                const int* d_seeds, int* d_nreb, int mode, double seg_evf, double seg_envf, double t0, double t1,
                double xmax, int nsteps, float* d_forces = nullptr) {
-    LaunchCfg cfg;
-    IGM_TRY(pick_cfg(c, pr.cm.natom, &cfg));
     AnnealArgs A;
     memset(&A, 0, sizeof(A));
     A.cm = pr.cm;
@@ -1401,17 +1914,40 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
             A.vinit = (const float*)pv;
         }
     }
-    A.nbr_stride = (size_t)pr.cm.nslice * pr.cm.kcap * 64;
     IGM_HIP_CHECK(c, hipMemsetAsync(pr.cm.work_counter, 0, sizeof(int), c->stream));
+    if (getenv("IGM_PROF")) {
+        void* pp;
+        IGM_TRY(workspace(c, "ms_prof", sizeof(unsigned long long) * 8, &pp));
+        IGM_HIP_CHECK(c, hipMemsetAsync(pp, 0, sizeof(unsigned long long) * 8, c->stream));
+        A.prof = (unsigned long long*)pp;
+    }
+    if (pr.big) {
+        auto kern = anneal_big_kernel<kBigNT>;
+        int grid = 0;
+        IGM_TRY(resident_grid(c, kern, kBigNT, 0, pr.cm.nstruct, &grid));
+        NList<float, int> L;
+        BigWs<float> W;
+        A.ws_stride = carve_ws<float>(nullptr, pr.cm.natom, pr.cm.ldn, pr.cm.kcap, kCellCapBig, true, true, &L, &W);
+        void* ws;
+        IGM_TRY(workspace(c, "ms_bigws", A.ws_stride * (size_t)grid, &ws));
+        A.ws = (unsigned char*)ws;
+        Timed tm(c, "anneal");
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBigNT), 0, c->stream, A);
+        IGM_HIP_CHECK(c, hipGetLastError());
+        return IGM_OK;
+    }
+    LaunchCfg cfg;
+    if (!lds_fits(pr.cm.natom, &cfg)) return fail(c, IGM_E_UNSUPPORTED, "no LDS configuration");
     IGM_DISPATCH_ALL({
-        const size_t lds = smem_bytes<float>(NT * BPT);
+        const size_t lds = kLdsBytes;
         auto kern = anneal_kernel<NT, BPT>;
         IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int grid = 0;
         IGM_TRY(resident_grid(c, kern, NT, lds, pr.cm.nstruct, &grid));
+        A.ws_stride = ((size_t)pr.cm.ldn * (pr.cm.kcap - kLdsListSlots) * 2 + 255) & ~size_t(255);
         void* ws;
-        IGM_TRY(workspace(c, "ms_nbr", sizeof(uint16_t) * A.nbr_stride * (size_t)grid, &ws));
-        A.nbr_ws = (uint16_t*)ws;
+        IGM_TRY(workspace(c, "ms_ldsovf", A.ws_stride * (size_t)grid, &ws));
+        A.ws = (unsigned char*)ws;
         Timed tm(c, "anneal");
         hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, c->stream, A);
         IGM_HIP_CHECK(c, hipGetLastError());
@@ -1422,8 +1958,6 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
 int run_cg(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, float* d_xyz, const float* d_vel,
            igm_opt_info* d_info, const int* d_nreb, int mode, double evf, double envf, float* d_forces,
            double* d_energies) {
-    LaunchCfg cfg;
-    IGM_TRY(pick_cfg(c, pr.cm.natom, &cfg));
     CGArgs A;
     memset(&A, 0, sizeof(A));
     A.cm = pr.cm;
@@ -1442,25 +1976,28 @@ int run_cg(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, float* d
     A.mode = mode;
     A.forces_out = d_forces;
     A.energies_out = d_energies;
-    A.nbr_stride = (size_t)pr.cm.nslice * pr.cm.kcap * 64;
     IGM_HIP_CHECK(c, hipMemsetAsync(pr.cm.work_counter, 0, sizeof(int), c->stream));
-    IGM_DISPATCH_ALL({
-        const size_t lds = smem_bytes<double>(NT * BPT);
-        auto kern = cg_kernel<NT, BPT>;
-        IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        int grid = 0;
-        IGM_TRY(resident_grid(c, kern, NT, lds, pr.cm.nstruct, &grid));
-        void* ws;
-        IGM_TRY(workspace(c, "ms_nbr", sizeof(uint16_t) * A.nbr_stride * (size_t)grid, &ws));
-        A.nbr_ws = (uint16_t*)ws;
-        void* vw;
-        A.vec_stride = 12 * (size_t)(NT * BPT);
-        IGM_TRY(workspace(c, "ms_cgvec", sizeof(double) * A.vec_stride * (size_t)grid, &vw));
-        A.vec_ws = (double*)vw;
-        Timed tm(c, mode == 0 ? "cg" : "forces");
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, c->stream, A);
-        IGM_HIP_CHECK(c, hipGetLastError());
-    })
+    constexpr int NT = 512;  // f64 force code: a 256-VGPR budget
+    const bool big = pr.big;
+    CgLds cg;
+    const size_t lds = carve_cg_lds(nullptr, pr.cm.ldn, big, &cg);
+    auto kern = big ? cg_kernel<NT, true> : cg_kernel<NT, false>;
+    IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int grid = 0;
+    IGM_TRY(resident_grid(c, kern, NT, lds, pr.cm.nstruct, &grid));
+    NList<double, int> L;
+    BigWs<double> W;
+    A.ws_stride = carve_ws<double>(nullptr, pr.cm.natom, pr.cm.ldn, pr.cm.kcap, big ? kCellCapBig : kCellCap, big,
+                                   false, &L, &W);
+    void *ws, *vw;
+    IGM_TRY(workspace(c, "ms_cgws", A.ws_stride * (size_t)grid, &ws));
+    A.ws = (unsigned char*)ws;
+    A.vec_stride = 15 * (size_t)pr.cm.ldn;
+    IGM_TRY(workspace(c, "ms_cgvec", sizeof(double) * A.vec_stride * (size_t)grid, &vw));
+    A.vec_ws = (double*)vw;
+    Timed tm(c, mode == 0 ? "cg" : "forces");
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, c->stream, A);
+    IGM_HIP_CHECK(c, hipGetLastError());
     return IGM_OK;
 }
 
@@ -1468,11 +2005,7 @@ int check_error(igm_ctx* c, const Prepared& pr) {
     int herr = 0;
     IGM_HIP_CHECK(c, hipMemcpyAsync(&herr, pr.cm.error, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
-    if (herr & 1)
-        return fail(c, IGM_E_OVERFLOW,
-                    "neighbour list overflow: an atom has more than %d neighbours within cutoff+skin; raise "
-                    "igm_mstep_params.neigh_capacity",
-                    pr.cm.kcap);
+    if (herr) return fail(c, IGM_E_HIP, "M-step kernel error bits 0x%x", herr);
     return IGM_OK;
 }
 
@@ -1615,4 +2148,19 @@ extern "C" int igm_velocity_create(igm_ctx* c, uint32_t flags, int32_t nseed, in
     IGM_HIP_CHECK(c, hipGetLastError());
     IGM_TRY(to_host(c, flags, v, (const float*)d_v, (size_t)nseed * natom * 3));
     return finish(c, flags);
+}
+
+/* Profiling aid (IGM_PROF=1 in the environment): cycle counters of the last LDS-path
+ * anneal launch summed over structures: {build, force, rest, steps, builds}. */
+extern "C" int igm_mstep_last_profile(igm_ctx* c, unsigned long long* out) {
+    if (!c || !out) return IGM_E_INVALID;
+    auto it = c->ws.find("ms_prof");
+    if (it == c->ws.end() || !it->second.first) {
+        memset(out, 0, sizeof(unsigned long long) * 5);
+        return IGM_OK;
+    }
+    IGM_HIP_CHECK(c, hipMemcpyAsync(out, it->second.first, sizeof(unsigned long long) * 5, hipMemcpyDeviceToHost,
+                                    c->stream));
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return IGM_OK;
 }

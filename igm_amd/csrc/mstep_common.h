@@ -162,6 +162,28 @@ __device__ __forceinline__ T bond_term(T r2, T r0, T k, bool lower, double& e) {
     return (r > T(0)) ? T(-2) * rk / r : T(0);
 }
 
+// branch-free f32 soft pair (the MD kernels): f/r multiplier, 0 outside the cutoff
+// or for coincident atoms; all candidates of a batch evaluate together
+__device__ __forceinline__ float soft_pair_bf(float r2, float rc, float evf) {
+    const float inv_pi = 0.318309886183790671537767526745f;
+    const float rinv = __frsqrt_rn(fmaxf(r2, 1.0e-30f));
+    const float r = r2 * rinv;
+    const float s = __builtin_amdgcn_sinf(0.5f * r * __frcp_rn(rc));  // sin(pi r / rc): v_sin takes revolutions
+    const float f = evf * rc * inv_pi * s * rinv;
+    return (r2 < rc * rc && r2 > 0.0f) ? f : 0.0f;
+}
+
+// branch-free harmonic upper/lower bound (f/r multiplier)
+template <typename T, bool EN>
+__device__ __forceinline__ T bond_term_bf(T r2, T r0, T k, bool lower, double& e) {
+    const T r = sqrt(r2);
+    const T dr = r - r0;
+    const bool active = lower ? (dr < T(0)) : (dr > T(0));
+    const T rk = k * dr;
+    if (EN && active) e += (double)rk * (double)dr;
+    return (active && r > T(0)) ? T(-2) * rk / r : T(0);
+}
+
 // ellipsoidal envelope on one atom; adds force, returns energy (if EN)
 template <typename T, bool EN>
 __device__ __forceinline__ void envelope_term(T x, T y, T z, T rad, T a, T b, T c, T k, T& fx, T& fy, T& fz,

@@ -3,6 +3,10 @@
 
   config B  2 Mb diploid (the demo index, 3008 beads), S structures, Hi-C pairs of
             the demo .hcs (tests/golden/demo_hic_pairs.npz), demo protocol.
+  config C  200 kb hg38 male diploid (15 453 haploid bins, 29 838 beads), radii from
+            occupancy 0.4 in a 5500 nm sphere (_preprocess.py:153-162), synthetic .hcs:
+            intra p = min(1, 0.9 |i-j|^-1) for |i-j| <= 200, inter density 1e-4 with
+            p ~ LogUniform(1e-3, 5e-2), default_rng(0).
   initial   RandomInit.generate_territories semantics (steps/RandomInit.py:207-240),
             R = init_radius, numpy.random.default_rng(1000 + sid) per structure.
 """
@@ -67,3 +71,89 @@ def hic_pairs_2mb(sigma):
         raise ValueError('the committed demo pairs cover sigma >= 0.02')
     m = d['p'] >= sigma
     return d['i'][m], d['j'][m], d['p'][m]
+
+
+# hg38 chromosome lengths (bp), chr1..chr22, chrX, chrY: the genome of the demo .hcs
+HG38_LENGTHS = [248956422, 242193529, 198295559, 190214555, 181538259, 170805979, 159345973, 145138636,
+                138394717, 133797422, 135086622, 133275309, 114364328, 107043718, 101991189, 90338345,
+                83257441, 80373285, 58617616, 64444167, 46709983, 50818468, 156040895, 57227415]
+
+
+def male_diploid_index(resolution, lengths=HG38_LENGTHS):
+    """alabtools make_diploid layout of a male genome (as in the demo index): copy 0
+    of chr1..chrY, then copy 1 of chr1..chr22; copy_index[h] = [h, h + nhap] for
+    autosomes, [h] for X and Y.  Returns dict(chrom, copy, start, end, chrom_sizes,
+    copy_ptr, copy_idx, nhap)."""
+    nb = [-(-L // resolution) for L in lengths]
+    hap_chrom = np.repeat(np.arange(len(lengths), dtype=np.int32), nb)
+    hap_start = np.concatenate([np.arange(n, dtype=np.int64) * resolution for n in nb])
+    hap_end = np.concatenate([np.minimum((np.arange(n, dtype=np.int64) + 1) * resolution, L)
+                              for n, L in zip(nb, lengths)])
+    nhap = len(hap_chrom)
+    auto = hap_chrom < 22
+    chrom = np.concatenate([hap_chrom, hap_chrom[auto]]).astype(np.int32)
+    copy = np.concatenate([np.zeros(nhap, np.int32), np.ones(int(auto.sum()), np.int32)])
+    start = np.concatenate([hap_start, hap_start[auto]])
+    end = np.concatenate([hap_end, hap_end[auto]])
+    second = np.full(nhap, -1, np.int64)
+    second[auto] = nhap + np.arange(int(auto.sum()))
+    ptr = np.zeros(nhap + 1, np.int32)
+    ptr[1:] = np.cumsum(1 + auto.astype(np.int32))
+    idx = np.empty(ptr[-1], np.int32)
+    idx[ptr[:-1]] = np.arange(nhap)
+    idx[ptr[:-1][auto] + 1] = second[auto]
+    chrom_sizes = np.concatenate([nb, nb[:22]]).astype(np.int64)
+    return dict(chrom=chrom, copy=copy, start=start, end=end, chrom_sizes=chrom_sizes, copy_ptr=ptr,
+                copy_idx=idx, nhap=nhap, hap_chrom=hap_chrom)
+
+
+def occupancy_radii(start, end, occupancy=0.4, nucleus_radius=5500.0):
+    """_preprocess.py:153-162: bead volume proportional to its bp size."""
+    vol = 4.0 / 3.0 * np.pi * nucleus_radius ** 3
+    bp = (end - start).astype(np.float64)
+    rho = occupancy * vol / bp.sum()
+    return ((rho * bp) / (4.0 / 3.0 * np.pi)) ** (1.0 / 3.0)
+
+
+def population_200kb(nstruct, first_sid=0, init_radius=7000.0):
+    """Config C: 200 kb hg38 male diploid, synthetic territories (same recipe as
+    population_2mb).  Same keys as population_2mb."""
+    ix = male_diploid_index(200000)
+    radii = occupancy_radii(ix['start'], ix['end']).astype(np.float32)
+    xyz = np.stack([territories(ix['chrom_sizes'], init_radius, 1000 + first_sid + s) for s in range(nstruct)])
+    return {'xyz': xyz, 'radii': radii, 'chrom': ix['chrom'], 'copy': ix['copy'], 'copy_ptr': ix['copy_ptr'],
+            'copy_idx': ix['copy_idx'], 'chrom_sizes': ix['chrom_sizes'], 'hap_chrom': ix['hap_chrom']}
+
+
+def hic_pairs_200kb(sigma, max_sep=200, inter_density=1e-4, seed=0):
+    """Synthetic 200 kb .hcs, upper triangle in CSR order,
+    entries with p >= sigma: (i, j, p) arrays."""
+    ix = male_diploid_index(200000)
+    hc = ix['hap_chrom']
+    n = ix['nhap']
+    rng = np.random.default_rng(seed)
+    ii, jj, pp = [], [], []
+    for d in range(1, max_sep + 1):
+        i = np.arange(n - d)
+        ok = hc[i] == hc[i + d]
+        ii.append(i[ok])
+        jj.append(i[ok] + d)
+        pp.append(np.full(int(ok.sum()), min(1.0, 0.9 / d), np.float32))
+    # inter-chromosomal entries: density inter_density of the inter pairs
+    sizes = np.bincount(hc)
+    n_inter = (n * n - int((sizes.astype(np.int64) ** 2).sum())) // 2
+    k = int(round(inter_density * n_inter))
+    a = rng.integers(0, n, 4 * k)
+    b = rng.integers(0, n, 4 * k)
+    lo, hi = np.minimum(a, b), np.maximum(a, b)
+    keep = hc[lo] != hc[hi]
+    key = np.unique(lo[keep].astype(np.int64) * n + hi[keep])[:k]
+    ii.append((key // n).astype(np.int64))
+    jj.append((key % n).astype(np.int64))
+    pp.append(np.exp(rng.uniform(np.log(1e-3), np.log(5e-2), len(key))).astype(np.float32))
+    i = np.concatenate(ii).astype(np.int32)
+    j = np.concatenate(jj).astype(np.int32)
+    p = np.concatenate(pp)
+    m = p >= sigma
+    order = np.lexsort((j[m], i[m]))
+    return i[m][order], j[m][order], p[m][order]

@@ -104,7 +104,9 @@ int igm_astep_update_plast(igm_ctx* ctx, uint32_t flags, igm_pair* pairs, int64_
  * Batched replacement of lammps.optimize (lammps.py:361-492): the protocol of
  * create_lammps_script (lammps.py:149-358) -- per stage: fix adapt of the soft
  * prefactor, envelope scaling, optional relax run, velocity create, temp/rescale
- * ramp, nve/limit -- followed by min_style cg.  One structure per workgroup.
+ * ramp, nve/limit -- followed by min_style cg.  One structure per workgroup:
+ * structures of up to 3072 atoms (2 Mb diploid) keep positions and the Verlet
+ * list in LDS; larger ones (200 kb diploid: 29 838 beads) keep them in HBM.
  */
 #define IGM_MAX_STAGES 16
 #define IGM_MAX_ENVELOPES 4
@@ -131,9 +133,13 @@ typedef struct {
     int32_t nenvelopes;
     double env_semiaxes[IGM_MAX_ENVELOPES][3];
     double env_k[IGM_MAX_ENVELOPES];
-    int32_t neigh_capacity; /* max neighbours per atom (0 = default)  */
-    int32_t flags;          /* reserved                                 */
+    int32_t neigh_capacity; /* HBM neighbour-list budget, mean entries per atom (0 = 64); atoms past
+                               the budget take their pair forces from a walk of the build-time cell grid */
+    int32_t flags;          /* IGM_MSTEP_* below                        */
 } igm_mstep_params;
+
+/* igm_mstep_params.flags */
+#define IGM_MSTEP_FORCE_GLOBAL 0x1 /* use the HBM-resident kernels even when a structure fits in LDS */
 
 /* atom flags (per atom, shared by all structures of a batch) */
 #define IGM_ATOM_BEAD 0x1u   /* takes part in the soft pair potential       */
@@ -200,6 +206,11 @@ int igm_mstep_md(igm_ctx* ctx, uint32_t flags, const igm_mstep_params* prm,
 int igm_velocity_create(igm_ctx* ctx, uint32_t flags, int32_t nseed, int32_t natom,
                         const uint32_t* atom_flags, const int32_t* seeds, double temperature,
                         float* v);
+
+/* Profiling aid: with IGM_PROF set in the environment, the LDS-path anneal kernel
+ * accumulates shader-clock cycles; out[5] = {neighbour builds, force phases, rest,
+ * force evaluations, builds} summed over the structures of the last launch. */
+int igm_mstep_last_profile(igm_ctx* ctx, unsigned long long* out);
 
 /* ---- M-step restraint assembly: Hi-C contact selection ---------------------
  * interHiC/intraHiC._apply (restraints/inter_hic.py:294-312, intra_hic.py) for
