@@ -35,13 +35,20 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--nstruct', type=int, default=1000, help='structures per GPU')
-    ap.add_argument('--sigma', type=float, default=0.02)
+    ap.add_argument('--config', choices=['B', 'C'], default='B',
+                    help='B: 2 Mb diploid (the N=1 metric workload); C: 200 kb diploid (29 838 beads)')
+    ap.add_argument('--nstruct', type=int, default=None, help='structures per GPU (B: 1000, C: 125)')
+    ap.add_argument('--sigma', type=float, default=None, help='Hi-C sigma (B: 0.02, C: 0.01)')
     ap.add_argument('--cpu-sample', type=int, default=16, help='structures in the CPU baseline sample (0: skip)')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--protocol-scale', type=float, default=1.0,
                     help='scale the MD step counts (only for smoke tests; the metric needs 1.0)')
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.nstruct is None:
+        a.nstruct = 1000 if a.config == 'B' else 125
+    if a.sigma is None:
+        a.sigma = 0.02 if a.config == 'B' else 0.01
+    return a
 
 
 def build_inputs(args, rank):
@@ -49,7 +56,7 @@ def build_inputs(args, rank):
     from igm_amd import synthetic as syn
     from igm_amd._lib import pair_dtype
     first = rank * args.nstruct
-    pop = syn.population_2mb(args.nstruct, first_sid=first)
+    pop = (syn.population_2mb if args.config == 'B' else syn.population_200kb)(args.nstruct, first_sid=first)
     atoms = M.Atoms(pop['radii'])
     natom = atoms.n
     xyz = np.zeros((args.nstruct, natom, 3), np.float32)
@@ -62,7 +69,7 @@ def build_inputs(args, rank):
         cap['mdsteps'] = [max(1, int(round(n * args.protocol_scale))) for n in cap['mdsteps']]
         cap['relax']['mdsteps'] = max(1, int(round(cap['relax']['mdsteps'] * args.protocol_scale)))
     prm = M.params_from_cfg({'optimization': {'optimizer_options': proto}}, [((5500.0,) * 3, 1.0)])
-    i, j, p = syn.hic_pairs_2mb(args.sigma)
+    i, j, p = (syn.hic_pairs_2mb if args.config == 'B' else syn.hic_pairs_200kb)(args.sigma)
     pairs = np.zeros(len(i), pair_dtype)
     pairs['i'], pairs['j'], pairs['pwish'], pairs['plast'] = i, j, p, 0.0
     return dict(pop=pop, atoms=atoms, xyz=xyz, chrom=chrom, poly=poly, prm=prm, pairs=pairs, first=first)
@@ -151,14 +158,18 @@ def main():
     achieved = float(np.mean(bytes_launch)) / (a_ms * 1e-3) / 1e9 if anneal_ms else 0.0
     if rank == 0:
         line = {
-            'metric': 'M-step structures/sec + A/M iteration wall-time, 2Mb diploid pop=1000 per GPU',
+            'metric': 'M-step structures/sec + A/M iteration wall-time (BASELINE.json), %s' % (
+                '2 Mb diploid pop=1000 per GPU (configs[1])' if args.config == 'B' else
+                '200 kb diploid pop=%d per GPU (configs[2] shard)' % args.nstruct),
             'value': value, 'unit': 'structures/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': ms_per_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': 'f32 (MD), f64 (CG, reductions)',
-            'data': 'synthetic: RandomInit territories default_rng(1000+sid), demo .hcs pairs sigma>=%g' % args.sigma,
-            'config': {'workload': 'B: 2 Mb diploid (3008 beads), Hi-C only, %d structures per GPU, demo '
-                                   'protocol%s' % (args.nstruct, '' if args.protocol_scale == 1.0 else
-                                                   ' x%g (NOT the metric)' % args.protocol_scale),
+            'data': 'synthetic: RandomInit territories default_rng(1000+sid), %s pairs sigma>=%g' % (
+                'demo .hcs' if args.config == 'B' else 'synthetic 200 kb .hcs (SURVEY 8d)', args.sigma),
+            'config': {'workload': '%s, Hi-C only, %d structures per GPU, demo protocol%s' % (
+                           'B: 2 Mb diploid (3008 beads)' if args.config == 'B' else 'C: 200 kb diploid (29 838 beads)',
+                           args.nstruct, '' if args.protocol_scale == 1.0 else
+                           ' x%g (NOT the metric)' % args.protocol_scale),
                        'nstruct_per_gpu': it.S_local, 'nstruct_total': total, 'sigma': args.sigma,
                        'npairs': int(it.npairs_total), 'parallelism': 'structures sharded, A-step pair-sharded'},
             'roofline': {'bound': 'hbm', 'kernel': 'anneal_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,

@@ -845,153 +845,365 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
     }
 }
 
-// The same protocol for structures too large for LDS: positions, Verlet list,
-// cell grid and per-atom v/f/last-build positions in the workgroup's HBM
-// workspace (SoA, coalesced); atoms a = t, t+NT, ...  The temperature rescale
-// factor is applied lazily when a velocity is next read.
-template <int NT>
-__global__ void __launch_bounds__(NT) anneal_big_kernel(AnnealArgs A) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[4096];
-    Carver cv(smem);
-    float* gp;
-    int* gn;
-    const Red R = carve_red<float>(cv, &gp, &gn);
-    const int t = threadIdx.x, lane = t & 63;
-    const int natom = A.cm.natom, ldn = A.cm.ldn;
+// ------------------------------------------------------------- population engine
+// Structures too large for one CU's LDS (the 200 kb model, 29 838 beads) are run as
+// ONE system: every step is a handful of launches over all atoms of all structures
+// (full-chip occupancy, memory-level parallelism), each structure keeping its own
+// HBM Verlet list, cell grid and temperature.  Blocks never straddle structures:
+// block b -> structure b / nbs, atoms (b % nbs) * kPopBS + t.  Per-structure sums
+// (temperature) go through per-block partials summed in a fixed order, so a run is
+// bitwise reproducible.
+constexpr int kPopBS = 256;
+
+struct PopArgs {
+    Common cm;
+    DevParams P;
+    unsigned char* ws;  // per structure: NList arrays + float4 positions (carve_ws)
+    size_t ws_stride;
+    float4* v4;         // (B, ldn)
+    float4* f4;         // (B, ldn)
+    float4* xb4;        // (B, ldn) positions at the last list build
+    float* gp;          // (B, 8) grid lo[3], inv[3]
+    int* gn;            // (B, 8) grid nb[3]
+    int* flag;          // (B) list rebuild needed
+    int* nrebuild;      // (B)
+    double* kep;        // (B, nbs) per-block kinetic-energy partials (2x KE, mass 1)
+    float* bbp;         // (B, nbs, 6) per-block bounding-box partials {max -x, -y, -z, max x, y, z}
+    int* ncell;         // (B) cells of the structure's current grid
+    int nbs;
+};
+
+__device__ __forceinline__ NList<float, int> pop_list(const PopArgs& A, int s, BigWs<float>* W) {
     NList<float, int> L;
+    carve_ws<float>(A.ws + (size_t)s * A.ws_stride, A.cm.natom, A.cm.ldn, A.cm.kcap, kCellCapBig, true, false, &L, W);
+    L.gp = A.gp + (size_t)s * 8;
+    L.gn = A.gn + (size_t)s * 8;
+    return L;
+}
+
+// XCD-aware block order: the grid (padded to a multiple of 8) is dealt round-robin
+// over the 8 XCDs, so logical block = (x % 8) * (grid / 8) + x / 8 keeps the blocks
+// of a structure on one XCD and its positions/lists in that XCD's L2.
+__device__ __forceinline__ int pop_block(const PopArgs& A) {
+    const int x = blockIdx.x, per = gridDim.x >> 3;
+    return (x & 7) * per + (x >> 3);
+}
+
+__global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float* xyz) {
+    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
     BigWs<float> W;
-    carve_ws<float>(A.ws + (size_t)blockIdx.x * A.ws_stride, natom, ldn, A.cm.kcap, kCellCapBig, true, true, &L, &W);
-    L.gp = gp;
-    L.gn = gn;
-    float4* pos = W.pos;
-    float *V = W.v, *F = W.f, *XB = W.xb;
-    for (;;) {
-        const int s = next_structure(A.cm, R.misc);
-        if (s >= A.cm.nstruct) break;
-        const float* xs = A.xyz + (size_t)s * natom * 3;
-        int nmob = 0;
-        for (int a = t; a < natom; a += NT) {
-            const uint32_t fl = A.cm.aflags[a];
-            nmob += (fl & IGM_ATOM_FIXED) ? 0 : 1;
-            const float r = A.cm.radii[a];
-            pos[a] = make_float4(xs[(size_t)a * 3], xs[(size_t)a * 3 + 1], xs[(size_t)a * 3 + 2],
-                                 (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                V[d * ldn + a] = 0.0f;
-                F[d * ldn + a] = 0.0f;
-                XB[d * ldn + a] = __int_as_float(0x7f800000);
-            }
+    pop_list(A, s, &W);
+    if (a == 0) {
+        A.flag[s] = 1;
+        A.nrebuild[s] = 0;
+    }
+    if (a >= A.cm.natom) return;
+    const size_t i = (size_t)s * A.cm.ldn + a;
+    const float* x = xyz + ((size_t)s * A.cm.natom + a) * 3;
+    const uint32_t fl = A.cm.aflags[a];
+    const float r = A.cm.radii[a];
+    W.pos[a] = make_float4(x[0], x[1], x[2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
+    A.v4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    A.f4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float inf = __int_as_float(0x7f800000);
+    A.xb4[i] = make_float4(inf, inf, inf, 0.f);
+}
+
+// velocities of a run: 'velocity create' of segment seg (vsrc = vinit + seg stride) or given
+__global__ void __launch_bounds__(kPopBS) pop_setvel_kernel(PopArgs A, const float* vsrc, size_t sstride) {
+    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
+    if (a >= A.cm.natom) return;
+    const float* v = vsrc + (size_t)s * sstride + (size_t)a * 3;
+    const bool mob = !(A.cm.aflags[a] & IGM_ATOM_FIXED);
+    A.v4[(size_t)s * A.cm.ldn + a] = mob ? make_float4(v[0], v[1], v[2], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+struct PopStep {
+    float dtv, dtf, vlim, vlimsq, trig;
+    int integrate;    // 0: neighbour check only (run setup)
+    int rescale;      // apply the temp/rescale of step `prev` first
+    int prev, nsteps;
+    float t0, t1, window, fraction;
+    double dof;
+};
+
+// temp/rescale factor of structure s at the end of step P.prev (fixed-order sum of partials)
+__device__ __forceinline__ float pop_factor(const PopArgs& A, const PopStep& S, int s, float* shared) {
+    if (threadIdx.x == 0) {
+        double ke = 0.0;
+        const double* kp = A.kep + (size_t)s * A.nbs;
+        for (int i = 0; i < A.nbs; ++i) ke += kp[i];
+        *shared = temp_rescale_factor(ke, S.dof, S.prev, S.nsteps, S.t0, S.t1, S.window, S.fraction);
+    }
+    __syncthreads();
+    return *shared;
+}
+
+// [end_of_step rescale of the previous step] + initial_integrate + the displacement check
+__global__ void __launch_bounds__(kPopBS) pop_kick_drift_kernel(PopArgs A, PopStep S) {
+    __shared__ float fac;
+    __shared__ float red[kPopBS / 64 * 6];
+    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
+    const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
+    BigWs<float> W;
+    pop_list(A, s, &W);
+    int moved = 0;
+    float mm[6] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
+    if (a < A.cm.natom) {
+        const size_t i = (size_t)s * A.cm.ldn + a;
+        float4 p = W.pos[a];
+        if (S.integrate && !(A.cm.aflags[a] & IGM_ATOM_FIXED)) {
+            float4 v = A.v4[i];
+            const float4 f = A.f4[i];
+            v.x *= factor;
+            v.y *= factor;
+            v.z *= factor;
+            kick_limit(v.x, v.y, v.z, f.x, f.y, f.z, S.dtf, S.vlim, S.vlimsq);
+            p.x += S.dtv * v.x;
+            p.y += S.dtv * v.y;
+            p.z += S.dtv * v.z;
+            A.v4[i] = v;
+            W.pos[a] = p;
         }
-        double cnt[1] = {(double)nmob};
-        block_sum<NT, 1>(cnt, R.red0);
-        const double dof = 3.0 * cnt[0] - 3.0;
-        __syncthreads();
-        const uint32_t* adj = A.cm.bonds.ent + A.cm.bonds.base[s];
-        const int* soff = A.cm.bonds.soff + (size_t)s * (A.cm.nslice + 1);
-        const int* deg = A.cm.bonds.deg + (size_t)s * natom;
-        const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
-        int nbuild = 0;
-        float pending = 1.0f;  // temp/rescale factor not yet applied to V
-        for (int seg = 0; seg < A.nseg; ++seg) {
-            const float* vsrc = A.mode == 1 ? A.vel + (size_t)s * natom * 3
-                                            : A.vinit + ((size_t)s * A.nseg + seg) * natom * 3;
-            for (int a = t; a < natom; a += NT) {
-                const bool mob = !(A.cm.aflags[a] & IGM_ATOM_FIXED);
-#pragma unroll
-                for (int d = 0; d < 3; ++d) V[d * ldn + a] = mob ? vsrc[(size_t)a * 3 + d] : 0.0f;
-            }
-            pending = 1.0f;
-            const int nsteps = A.seg_steps[seg];
-            const float evf = A.seg_evf[seg], envf = A.seg_envf[seg];
-            const float t0 = A.seg_t0[seg], t1 = A.seg_t1[seg];
-            const float dtv = A.dt, dtf = 0.5f * A.dt;
-            const float vlim = A.seg_xmax[seg] / dtv;
-            const float vlimsq = vlim * vlim;
-            const float trig = 0.25f * A.P.skin * A.P.skin;
-            for (int step = 0; step <= nsteps; ++step) {
-                int moved = 0;
-                for (int a = t; a < natom; a += NT) {
-                    float4 p = pos[a];
-                    if (step > 0 && !(A.cm.aflags[a] & IGM_ATOM_FIXED)) {
-                        float vx = V[a] * pending, vy = V[ldn + a] * pending, vz = V[2 * ldn + a] * pending;
-                        kick_limit(vx, vy, vz, F[a], F[ldn + a], F[2 * ldn + a], dtf, vlim, vlimsq);
-                        V[a] = vx;
-                        V[ldn + a] = vy;
-                        V[2 * ldn + a] = vz;
-                        p.x += dtv * vx;
-                        p.y += dtv * vy;
-                        p.z += dtv * vz;
-                        pos[a] = p;
-                    }
-                    if (p.w >= 0.0f) {
-                        const float ddx = p.x - XB[a], ddy = p.y - XB[ldn + a], ddz = p.z - XB[2 * ldn + a];
-                        moved |= !(ddx * ddx + ddy * ddy + ddz * ddz <= trig);
-                    }
-                }
-                pending = 1.0f;
-                if (__syncthreads_or(moved)) {
-                    build_nlist<float, NT, int>(natom, pos, L, A.P.cut_list, R);
-                    ++nbuild;
-                    for (int a = t; a < natom; a += NT) {
-                        const float4 p = pos[a];
-                        XB[a] = p.x;
-                        XB[ldn + a] = p.y;
-                        XB[2 * ldn + a] = p.z;
-                    }
-                }
-                for (int a = t; a < natom; a += NT) {
-                    double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
-                    float fx, fy, fz;
-                    const BondView B{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
-                    atom_force<float, false, int>(a, pos[a], A.cm.aflags[a], pos, L, XB[a], XB[ldn + a],
-                                                  XB[2 * ldn + a], B, A.P, evf, envf, fx, fy, fz, ep, eb, ee);
-                    F[a] = fx;
-                    F[ldn + a] = fy;
-                    F[2 * ldn + a] = fz;
-                }
-                if (step == 0) {
-                    __syncthreads();
-                    continue;
-                }
-                double ts[1] = {0.0};
-                for (int a = t; a < natom; a += NT) {
-                    if (A.cm.aflags[a] & IGM_ATOM_FIXED) continue;
-                    float vx = V[a], vy = V[ldn + a], vz = V[2 * ldn + a];
-                    kick_limit(vx, vy, vz, F[a], F[ldn + a], F[2 * ldn + a], dtf, vlim, vlimsq);
-                    V[a] = vx;
-                    V[ldn + a] = vy;
-                    V[2 * ldn + a] = vz;
-                    ts[0] += (double)(vx * vx) + (double)(vy * vy) + (double)(vz * vz);
-                }
-                block_sum<NT, 1>(ts, (step & 1) ? R.red1 : R.red0);
-                pending = temp_rescale_factor(ts[0], dof, step, nsteps, t0, t1, A.t_window, A.t_fraction);
-            }
-            if (pending != 1.0f) {
-                for (int a = t; a < natom; a += NT)
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) V[d * ldn + a] *= pending;
-                pending = 1.0f;
-            }
+        if (p.w >= 0.0f) {
+            const float4 b = A.xb4[i];
+            const float dx = p.x - b.x, dy = p.y - b.y, dz = p.z - b.z;
+            moved = !(dx * dx + dy * dy + dz * dz <= S.trig);
+            mm[0] = -p.x;
+            mm[1] = -p.y;
+            mm[2] = -p.z;
+            mm[3] = p.x;
+            mm[4] = p.y;
+            mm[5] = p.z;
         }
-        __syncthreads();
-        float* xo = A.xyz + (size_t)s * natom * 3;
-        float* vo = A.vel + (size_t)s * natom * 3;
-        for (int a = t; a < natom; a += NT) {
-            const float4 p = pos[a];
-            xo[(size_t)a * 3] = p.x;
-            xo[(size_t)a * 3 + 1] = p.y;
-            xo[(size_t)a * 3 + 2] = p.z;
+    }
+    // this block's bounding box of the beads (for a list build of the structure)
 #pragma unroll
-            for (int d = 0; d < 3; ++d) vo[(size_t)a * 3 + d] = V[d * ldn + a];
-            if (A.forces_out) {
-                float* fo3 = A.forces_out + ((size_t)s * natom + a) * 3;
+    for (int d = 0; d < 6; ++d)
 #pragma unroll
-                for (int d = 0; d < 3; ++d) fo3[d] = F[d * ldn + a];
-            }
+        for (int off = 32; off > 0; off >>= 1) mm[d] = fmaxf(mm[d], __shfl_xor(mm[d], off));
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int d = 0; d < 6; ++d) red[(threadIdx.x >> 6) * 6 + d] = mm[d];
+    if (__syncthreads_or(moved) && threadIdx.x == 0) atomicOr(&A.flag[s], 1);
+    if (threadIdx.x < 6) {
+        float m = red[threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < kPopBS / 64; ++w) m = fmaxf(m, red[w * 6 + threadIdx.x]);
+        A.bbp[((size_t)s * A.nbs + lb % A.nbs) * 6 + threadIdx.x] = m;
+    }
+}
+
+// ---- population-wide Verlet-list build of the flagged structures (the steps of
+// build_nlist, each over all atoms / cells of every flagged structure):
+//   grid (+ zero counts) | count | scan | scatter | per-cell sort | fill
+__global__ void __launch_bounds__(256) pop_grid_kernel(PopArgs A) {
+    __shared__ int nc;
+    const int s = blockIdx.x;
+    if (!A.flag[s]) return;
+    if (threadIdx.x == 0) {
+        float mm[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) mm[d] = -3.0e38f;
+        const float* bp = A.bbp + (size_t)s * A.nbs * 6;
+        for (int b = 0; b < A.nbs; ++b)
+#pragma unroll
+            for (int d = 0; d < 6; ++d) mm[d] = fmaxf(mm[d], bp[b * 6 + d]);
+        // the grid of build_nlist: cells of side >= cut_list, at most kCellCapBig
+        float ext[3], vol = 1.0f;
+        const float cut = A.P.cut_list;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            ext[d] = mm[3 + d] + mm[d];
+            if (!(ext[d] >= 0.0f)) ext[d] = 0.0f;
+            vol *= fmaxf(ext[d], cut);
         }
-        if (t == 0 && A.nrebuild) A.nrebuild[s] = nbuild;
-        __syncthreads();
+        float cs = cut;
+        if (vol / (cs * cs * cs) > (float)kCellCapBig) cs = cbrtf(vol / (float)kCellCapBig) * 1.0001f;
+        float* gp = A.gp + (size_t)s * 8;
+        int* gn = A.gn + (size_t)s * 8;
+        int n = 1;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            int nbd = (int)floorf(ext[d] / cs);
+            if (nbd < 1) nbd = 1;
+            gp[d] = -mm[d];
+            gp[3 + d] = ext[d] > 0.0f ? (float)nbd / ext[d] : 0.0f;
+            gn[d] = nbd;
+            n *= nbd;
+        }
+        A.ncell[s] = n;
+        nc = n;
+    }
+    __syncthreads();
+    BigWs<float> W;
+    const NList<float, int> L = pop_list(A, s, &W);
+    for (int c = threadIdx.x; c <= nc; c += 256) L.scratch[c] = 0;
+}
+
+__global__ void __launch_bounds__(kPopBS) pop_count_kernel(PopArgs A) {
+    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
+    if (!A.flag[s] || a >= A.cm.natom) return;
+    BigWs<float> W;
+    const NList<float, int> L = pop_list(A, s, &W);
+    const float4 p = W.pos[a];
+    if (!(p.w >= 0.0f)) return;
+    int* cnt = L.scratch;
+    int* slot = cnt + A.ncell[s] + 1;
+    slot[a] = atomicAdd(&cnt[cell_index<float>(p.x, p.y, p.z, L.gp, L.gp + 3, L.gn)], 1);
+}
+
+__global__ void __launch_bounds__(1024) pop_scan_kernel(PopArgs A) {
+    __shared__ int wsum[kMaxWaves];
+    const int s = blockIdx.x;
+    if (!A.flag[s]) return;
+    BigWs<float> W;
+    const NList<float, int> L = pop_list(A, s, &W);
+    const int n = A.ncell[s];
+    block_scan<1024, int, int>(L.scratch, L.scratch, n, wsum);
+    for (int c = threadIdx.x; c <= n; c += 1024) L.cell[c] = L.scratch[c];
+}
+
+__global__ void __launch_bounds__(kPopBS) pop_scatter_kernel(PopArgs A) {
+    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
+    if (!A.flag[s] || a >= A.cm.natom) return;
+    BigWs<float> W;
+    const NList<float, int> L = pop_list(A, s, &W);
+    const float4 p = W.pos[a];
+    if (!(p.w >= 0.0f)) return;
+    const int* slot = L.scratch + A.ncell[s] + 1;
+    L.sorted[L.cell[cell_index<float>(p.x, p.y, p.z, L.gp, L.gp + 3, L.gn)] + slot[a]] = (uint16_t)a;
+}
+
+constexpr int kPopCellBlocks = kCellCapBig / 256;
+
+__global__ void __launch_bounds__(256) pop_cellsort_kernel(PopArgs A) {
+    const int s = blockIdx.x / kPopCellBlocks, c = (blockIdx.x % kPopCellBlocks) * 256 + threadIdx.x;
+    if (!A.flag[s] || c >= A.ncell[s]) return;
+    BigWs<float> W;
+    const NList<float, int> L = pop_list(A, s, &W);
+    const int beg = L.cell[c], end = L.cell[c + 1];
+    for (int i = beg + 1; i < end; ++i) {  // deterministic order inside the cell
+        const uint16_t v = L.sorted[i];
+        int k = i - 1;
+        while (k >= beg && L.sorted[k] > v) {
+            L.sorted[k + 1] = L.sorted[k];
+            --k;
+        }
+        L.sorted[k + 1] = v;
+    }
+}
+
+__global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
+    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
+    if (!A.flag[s] || a >= A.cm.natom) return;
+    BigWs<float> W;
+    const NList<float, int> L = pop_list(A, s, &W);
+    const float4 p0 = W.pos[a];
+    A.xb4[(size_t)s * A.cm.ldn + a] = make_float4(p0.x, p0.y, p0.z, 0.f);
+    const float cut2 = A.P.cut_list * A.P.cut_list;
+    const int cap = L.kl + L.kg;
+    int k = 0;
+    if (p0.w >= 0.0f) {
+        walk27(cell_index<float>(p0.x, p0.y, p0.z, L.gp, L.gp + 3, L.gn), L.cell, L.sorted, L.gn,
+               [&](int j, bool ok) {
+                   const float4 p = W.pos[j];
+                   const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
+                   const bool in = ok && j != a && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
+                   if (in && k < cap) L.gell[((size_t)(a >> 6) * L.kg + k) * 64 + (a & 63)] = (uint16_t)j;
+                   k += in ? 1 : 0;
+               });
+    }
+    L.nnb[a] = (uint16_t)(k <= cap ? k : kNnbWalk);
+}
+
+__global__ void __launch_bounds__(kPopBS) pop_forces_kernel(PopArgs A, float evf, float envf) {
+    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
+    if (a == 0 && A.flag[s]) {  // the structure's list was rebuilt this step
+        A.flag[s] = 0;
+        A.nrebuild[s] += 1;
+    }
+    if (a >= A.cm.natom) return;
+    BigWs<float> W;
+    const NList<float, int> L = pop_list(A, s, &W);
+    const size_t i = (size_t)s * A.cm.ldn + a;
+    const uint32_t* adj = A.cm.bonds.ent + A.cm.bonds.base[s];
+    const int* soff = A.cm.bonds.soff + (size_t)s * (A.cm.nslice + 1);
+    const BondView B{adj + soff[a >> 6] + (a & 63), A.cm.bonds.types + A.cm.bonds.tbase[s], nullptr, nullptr,
+                     A.cm.bonds.deg[(size_t)s * A.cm.natom + a]};
+    const float4 b = A.xb4[i];
+    double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
+    float fx, fy, fz;
+    atom_force<float, false, int>(a, W.pos[a], A.cm.aflags[a], W.pos, L, b.x, b.y, b.z, B, A.P, evf, envf, fx, fy,
+                                  fz, ep, eb, ee);
+    A.f4[i] = make_float4(fx, fy, fz, 0.f);
+}
+
+// final_integrate + this block's kinetic-energy partial
+__global__ void __launch_bounds__(kPopBS) pop_kick_kernel(PopArgs A, PopStep S) {
+    __shared__ double red[kPopBS / 64];
+    const int lb = pop_block(A), s = lb / A.nbs, blk = lb % A.nbs, a = blk * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
+    double ke = 0.0;
+    if (a < A.cm.natom && !(A.cm.aflags[a] & IGM_ATOM_FIXED)) {
+        const size_t i = (size_t)s * A.cm.ldn + a;
+        float4 v = A.v4[i];
+        const float4 f = A.f4[i];
+        kick_limit(v.x, v.y, v.z, f.x, f.y, f.z, S.dtf, S.vlim, S.vlimsq);
+        A.v4[i] = v;
+        ke = (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ke += __shfl_xor(ke, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ke;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < kPopBS / 64; ++w) t += red[w];
+        A.kep[(size_t)s * A.nbs + blk] = t;
+    }
+}
+
+// end of a run: the last step's rescale, then (optionally) the outputs
+__global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S, float* xyz, float* vel,
+                                                            float* forces_out) {
+    __shared__ float fac;
+    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct) return;
+    const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
+    if (a >= A.cm.natom) return;
+    const size_t i = (size_t)s * A.cm.ldn + a;
+    float4 v = A.v4[i];
+    v.x *= factor;
+    v.y *= factor;
+    v.z *= factor;
+    A.v4[i] = v;
+    if (!xyz) return;  // more runs follow
+    BigWs<float> W;
+    pop_list(A, s, &W);
+    const float4 p = W.pos[a];
+    float* xo = xyz + ((size_t)s * A.cm.natom + a) * 3;
+    xo[0] = p.x;
+    xo[1] = p.y;
+    xo[2] = p.z;
+    float* vo = vel + ((size_t)s * A.cm.natom + a) * 3;
+    vo[0] = v.x;
+    vo[1] = v.y;
+    vo[2] = v.z;
+    if (forces_out) {
+        const float4 f = A.f4[i];
+        float* fo = forces_out + ((size_t)s * A.cm.natom + a) * 3;
+        fo[0] = f.x;
+        fo[1] = f.y;
+        fo[2] = f.z;
     }
 }
 
@@ -1810,7 +2022,7 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
     while ((size_t)out->cm.ldn * kcap * 2 < build_scratch_bytes(kCellCapBig, out->cm.ldn)) ++kcap;
     out->cm.kcap = kcap;
     LaunchCfg cfg;
-    out->big = (prm->flags & IGM_MSTEP_FORCE_GLOBAL) || !lds_fits(natom, &cfg);
+    out->big = (prm->flags & IGM_MSTEP_FORCE_GLOBAL) || getenv("IGM_FORCE_POP") || !lds_fits(natom, &cfg);
     out->P = P;
     return IGM_OK;
 }
@@ -1844,7 +2056,100 @@ int resident_grid(igm_ctx* c, KernelT kernel, int nt, size_t lds, int nstruct, i
     return IGM_OK;
 }
 
-constexpr int kBigNT = 512;
+
+// The population engine (HBM path): per step  kick+drift+check | list builds | forces |
+// kick + temperature partials, over every atom of every structure.
+int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
+    const int S = pr.cm.nstruct, N = pr.cm.natom, ldn = pr.cm.ldn;
+    PopArgs Q;
+    memset(&Q, 0, sizeof(Q));
+    Q.cm = pr.cm;
+    Q.P = pr.P;
+    Q.nbs = (N + kPopBS - 1) / kPopBS;
+    NList<float, int> L;
+    BigWs<float> W;
+    Q.ws_stride = carve_ws<float>(nullptr, N, ldn, pr.cm.kcap, kCellCapBig, true, false, &L, &W);
+    void *ws, *pv, *pf, *pb, *pgp, *pgn, *pfl, *pke, *pbb, *pnc;
+    IGM_TRY(workspace(c, "pop_ws", Q.ws_stride * (size_t)S, &ws));
+    IGM_TRY(workspace(c, "pop_v", sizeof(float4) * (size_t)S * ldn, &pv));
+    IGM_TRY(workspace(c, "pop_f", sizeof(float4) * (size_t)S * ldn, &pf));
+    IGM_TRY(workspace(c, "pop_xb", sizeof(float4) * (size_t)S * ldn, &pb));
+    IGM_TRY(workspace(c, "pop_gp", sizeof(float) * 8 * (size_t)S, &pgp));
+    IGM_TRY(workspace(c, "pop_gn", sizeof(int) * 8 * (size_t)S, &pgn));
+    IGM_TRY(workspace(c, "pop_flag", sizeof(int) * (size_t)S, &pfl));
+    IGM_TRY(workspace(c, "pop_ke", sizeof(double) * (size_t)S * Q.nbs, &pke));
+    IGM_TRY(workspace(c, "pop_bb", sizeof(float) * 6 * (size_t)S * Q.nbs, &pbb));
+    IGM_TRY(workspace(c, "pop_nc", sizeof(int) * (size_t)S, &pnc));
+    void* pnr = A.nrebuild;
+    if (!pnr) IGM_TRY(workspace(c, "pop_nreb", sizeof(int) * (size_t)S, &pnr));
+    Q.ws = (unsigned char*)ws;
+    Q.v4 = (float4*)pv;
+    Q.f4 = (float4*)pf;
+    Q.xb4 = (float4*)pb;
+    Q.gp = (float*)pgp;
+    Q.gn = (int*)pgn;
+    Q.flag = (int*)pfl;
+    Q.kep = (double*)pke;
+    Q.bbp = (float*)pbb;
+    Q.ncell = (int*)pnc;
+    Q.nrebuild = (int*)pnr;
+    // dof of group nonfixed (flags are shared by the structures)
+    std::vector<uint32_t> fl(N);
+    IGM_HIP_CHECK(c, hipMemcpyAsync(fl.data(), pr.cm.aflags, sizeof(uint32_t) * N, hipMemcpyDeviceToHost, c->stream));
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    int nmob = 0;
+    for (int i = 0; i < N; ++i) nmob += (fl[i] & IGM_ATOM_FIXED) ? 0 : 1;
+    const dim3 grid((S * Q.nbs + 7) & ~7), blk(kPopBS);  // padded for pop_block
+    Timed tm(c, "anneal");
+    hipLaunchKernelGGL(pop_load_kernel, grid, blk, 0, c->stream, Q, (const float*)A.xyz);
+    if (A.nseg == 0) {  // no runs (CG only): velocities 0, positions unchanged
+        PopStep st;
+        memset(&st, 0, sizeof(st));
+        hipLaunchKernelGGL(pop_finish_kernel, grid, blk, 0, c->stream, Q, st, A.xyz, A.vel, A.forces_out);
+    }
+    for (int seg = 0; seg < A.nseg; ++seg) {
+        const float* vsrc = A.mode == 1 ? A.vel : A.vinit + (size_t)seg * N * 3;
+        const size_t sstride = A.mode == 1 ? (size_t)N * 3 : (size_t)A.nseg * N * 3;
+        hipLaunchKernelGGL(pop_setvel_kernel, grid, blk, 0, c->stream, Q, vsrc, sstride);
+        PopStep st;
+        memset(&st, 0, sizeof(st));
+        st.dtv = A.dt;
+        st.dtf = 0.5f * A.dt;
+        st.vlim = A.seg_xmax[seg] / A.dt;
+        st.vlimsq = st.vlim * st.vlim;
+        st.trig = 0.25f * pr.P.skin * pr.P.skin;
+        st.nsteps = A.seg_steps[seg];
+        st.t0 = A.seg_t0[seg];
+        st.t1 = A.seg_t1[seg];
+        st.window = A.t_window;
+        st.fraction = A.t_fraction;
+        st.dof = 3.0 * nmob - 3.0;
+        const float evf = A.seg_evf[seg], envf = A.seg_envf[seg];
+        for (int step = 0; step <= st.nsteps; ++step) {
+            st.integrate = step > 0;
+            st.rescale = step > 1;
+            st.prev = step - 1;
+            hipLaunchKernelGGL(pop_kick_drift_kernel, grid, blk, 0, c->stream, Q, st);
+            // list builds of the flagged structures (every launch exits at once for the others)
+            hipLaunchKernelGGL(pop_grid_kernel, dim3(S), dim3(256), 0, c->stream, Q);
+            hipLaunchKernelGGL(pop_count_kernel, grid, blk, 0, c->stream, Q);
+            hipLaunchKernelGGL(pop_scan_kernel, dim3(S), dim3(1024), 0, c->stream, Q);
+            hipLaunchKernelGGL(pop_scatter_kernel, grid, blk, 0, c->stream, Q);
+            hipLaunchKernelGGL(pop_cellsort_kernel, dim3(S * kPopCellBlocks), dim3(256), 0, c->stream, Q);
+            hipLaunchKernelGGL(pop_fill_kernel, grid, blk, 0, c->stream, Q);
+            hipLaunchKernelGGL(pop_forces_kernel, grid, blk, 0, c->stream, Q, evf, envf);
+            if (step > 0) hipLaunchKernelGGL(pop_kick_kernel, grid, blk, 0, c->stream, Q, st);
+        }
+        IGM_HIP_CHECK(c, hipGetLastError());
+        st.rescale = st.nsteps > 0;
+        st.prev = st.nsteps;
+        const bool last = seg + 1 == A.nseg;
+        hipLaunchKernelGGL(pop_finish_kernel, grid, blk, 0, c->stream, Q, st, last ? A.xyz : nullptr,
+                           last ? A.vel : nullptr, last ? A.forces_out : nullptr);
+    }
+    IGM_HIP_CHECK(c, hipGetLastError());
+    return IGM_OK;
+}
 
 int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, float* d_xyz, float* d_vel,
                const int* d_seeds, int* d_nreb, int mode, double seg_evf, double seg_envf, double t0, double t1,
@@ -1921,21 +2226,7 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
         IGM_HIP_CHECK(c, hipMemsetAsync(pp, 0, sizeof(unsigned long long) * 8, c->stream));
         A.prof = (unsigned long long*)pp;
     }
-    if (pr.big) {
-        auto kern = anneal_big_kernel<kBigNT>;
-        int grid = 0;
-        IGM_TRY(resident_grid(c, kern, kBigNT, 0, pr.cm.nstruct, &grid));
-        NList<float, int> L;
-        BigWs<float> W;
-        A.ws_stride = carve_ws<float>(nullptr, pr.cm.natom, pr.cm.ldn, pr.cm.kcap, kCellCapBig, true, true, &L, &W);
-        void* ws;
-        IGM_TRY(workspace(c, "ms_bigws", A.ws_stride * (size_t)grid, &ws));
-        A.ws = (unsigned char*)ws;
-        Timed tm(c, "anneal");
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBigNT), 0, c->stream, A);
-        IGM_HIP_CHECK(c, hipGetLastError());
-        return IGM_OK;
-    }
+    if (pr.big) return run_anneal_pop(c, pr, A);
     LaunchCfg cfg;
     if (!lds_fits(pr.cm.natom, &cfg)) return fail(c, IGM_E_UNSUPPORTED, "no LDS configuration");
     IGM_DISPATCH_ALL({
