@@ -1,0 +1,180 @@
+"""ORACLE (test infrastructure only -- never imported by the product path):
+NumPy restatements of the configuration D/E A-steps of the reference, operation by
+operation with NumPy-1.x promotion, pinned against the golden vectors that
+tests/golden/make_golden_asteps.py produced by running the reference itself.
+
+  damid_actdist          steps/DamidActivationDistanceStep.py:39-76,362-471 (+ the
+                         "%6d %.5f %.5f" text round trip of task()/reduce(), :35,:286,:308)
+  fish_radial/fish_pair  steps/FishAssignmentStep.py:23-77,188-242
+  sprite_cluster_rg2     cython_compiled/sprite.pyx:104-283 with get_rg2s_cpp
+                         (cpp_sprite_assignment.cpp:49-143)
+  keep_best              steps/SpriteAssignmentStep.py:138-143
+"""
+import numpy as np
+
+f32 = np.float32
+
+
+def _clean(pij, pexist):
+    """cleanProbability (DamidActivationDistanceStep.py:362-372).  Under NumPy 1.x an
+    np.float32 scalar combined with a Python float or int promotes to float64 (NumPy 2
+    would stay in float32, so the casts are explicit); max(0, x) returns 0 if x <= 0."""
+    pij, pexist = float(pij), float(pexist)
+    if pexist < 1:
+        pclean = (pij - pexist) / (1.0 - pexist)
+    else:
+        pclean = pij
+    return max(0, pclean)
+
+
+def damid_d2(x, r, contact_range, shape, param):
+    """snormsq_sphere / snormsq_ellipse (py:39-76) as get_damid_actdist_I calls them
+    (R = param * (1 - contact_range), :436-438): x (S, 3) f32 -> (S,) f32 values.
+    NumPy 1.x value-based casting: the float64 scalar divisor is cast to float32 and
+    the division runs in float32 (written out explicitly for NumPy 2)."""
+    x = np.asarray(x, np.float32)
+    R = np.array(param, np.float64) * (1 - contact_range)
+    sq = np.square(x)
+    if shape == 'sphere':
+        D = f32((float(R) - float(r)) ** 2)
+        return ((sq[:, 0] + sq[:, 1]) + sq[:, 2]) / D
+    a, b, c = (float(v) - float(r) for v in R)
+    return (sq[:, 0] / f32(a * a) + sq[:, 1] / f32(b * b)) + sq[:, 2] / f32(c * c)
+
+
+def damid_actdist(crd, radii, copy_ptr, copy_idx, loci, profile, plast, it_corr, contact_range=0.05,
+                  shape='sphere', param=5000.0):
+    """Rows {loc, dist, prob} task() writes for the loci (in order), after the text
+    round trip.  crd: bead-major (N, S, 3) f32."""
+    rows = []
+    S = crd.shape[1]
+    for I in loci:
+        ii = [int(v) for v in copy_idx[copy_ptr[I]:copy_ptr[I + 1]]]
+        nc = len(ii)
+        p_exp, pl = f32(profile[I]), f32(plast[I])  # setup() stores (I, p_exp, plast) as float32 (:211-217)
+        r = radii[ii[0]]
+        d_sq = np.empty(nc * S)
+        for i in range(nc):
+            d_sq[i * S:(i + 1) * S] = damid_d2(crd[ii[i]], r, contact_range, shape, param)
+        d_sq[::-1].sort()  # descending (:444)
+        if it_corr == 1:
+            pnow = float(np.count_nonzero(d_sq >= 1.0)) / (S * nc)
+            p = _clean(p_exp, _clean(pnow, pl))
+        else:
+            p = float(p_exp)
+        ad = 2
+        if p > 0:
+            o = min(nc * S - 1, int(np.round(np.float64(nc * S) * p)))  # round half to even
+            ad = float(np.sqrt(d_sq[o]))
+        for i in ii:
+            line = '%6d %.5f %.5f' % (i, ad, p)
+            a, b, c = line.split()
+            rows.append((int(a), f32(float(b)), f32(float(c))))
+    out = np.zeros(len(rows), [('loc', 'i4'), ('dist', 'f4'), ('prob', 'f4')])
+    if rows:
+        out['loc'], out['dist'], out['prob'] = zip(*rows)
+    return out
+
+
+def _rank(v):
+    """argsort(argsort(v)) (FishAssignmentStep.py:74-75) with ties in index order."""
+    order = np.argsort(v, kind='stable')
+    r = np.empty(len(v), np.int64)
+    r[order] = np.arange(len(v))
+    return r
+
+
+def fish_radial(crd, copy_ptr, copy_idx, probes, tmin, tmax):
+    """get_rad_dists + get_min_max_and_idx + target[idx] (py:44-77, 218-242) for every
+    probe; every copy of the probe (the reference reads ii[0], ii[1] only)."""
+    S = crd.shape[1]
+    out_min = np.zeros((len(probes), S), np.float32)
+    out_max = np.zeros((len(probes), S), np.float32)
+    dmin = np.zeros((len(probes), S))
+    dmax = np.zeros((len(probes), S))
+    for q, pr in enumerate(probes):
+        ii = copy_idx[copy_ptr[pr]:copy_ptr[pr + 1]]
+        d = np.stack([np.linalg.norm(crd[i], axis=1) for i in ii]).astype(np.float64)
+        dmin[q], dmax[q] = d.min(0), d.max(0)
+        out_min[q] = tmin[q][_rank(dmin[q])]
+        out_max[q] = tmax[q][_rank(dmax[q])]
+    return out_min, out_max, dmin, dmax
+
+
+def fish_pair(crd, copy_ptr, copy_idx, pairs, tmin, tmax):
+    """The pair path with every copy pair's distance (get_pair_dists' documented
+    intent; the reference never advances its row counter, defect D4)."""
+    S = crd.shape[1]
+    out_min = np.zeros((len(pairs), S), np.float32)
+    out_max = np.zeros((len(pairs), S), np.float32)
+    dmin = np.zeros((len(pairs), S))
+    dmax = np.zeros((len(pairs), S))
+    for q, (i, j) in enumerate(pairs):
+        ii = copy_idx[copy_ptr[i]:copy_ptr[i + 1]]
+        jj = copy_idx[copy_ptr[j]:copy_ptr[j + 1]]
+        d = np.stack([np.linalg.norm(crd[a] - crd[b], axis=1) for a in ii for b in jj]).astype(np.float64)
+        dmin[q], dmax[q] = d.min(0), d.max(0)
+        out_min[q] = tmin[q][_rank(dmin[q])]
+        out_max[q] = tmax[q][_rank(dmax[q])]
+    return out_min, out_max, dmin, dmax
+
+
+def rg2_f32(pts):
+    """gyration_radius_sq (cpp_sprite_assignment.cpp:49-61) in float32, left to right."""
+    n = len(pts)
+    m = [f32(0), f32(0), f32(0)]
+    for p in pts:
+        m = [f32(m[d] + p[d]) for d in range(3)]
+    m = [f32(m[d] / f32(n)) for d in range(3)]
+    rg = f32(0)
+    for p in pts:
+        dx, dy, dz = f32(p[0] - m[0]), f32(p[1] - m[1]), f32(p[2] - m[2])
+        rg = f32(rg + f32(f32(f32(dx * dx) + f32(dy * dy)) + f32(dz * dz)))
+    return f32(rg / f32(n))
+
+
+def sprite_cluster_rg2(crd, hap_chrom, copy_ptr, copy_idx, cluster, reps, structs=None):
+    """compute_gyration_radius (sprite.pyx:104-283) with the per-chromosome
+    representatives given (they are np.random.choice draws in the reference, D9).
+    Returns rg2s (S,) f32 and selected beads (S, len(cluster))."""
+    cluster = np.sort(np.asarray(cluster))
+    S = crd.shape[1]
+    structs = range(S) if structs is None else structs
+    ci = lambda h: [int(v) for v in copy_idx[copy_ptr[h]:copy_ptr[h + 1]]]
+    cchroms = hap_chrom[cluster]
+    rg = np.zeros(S, np.float32)
+    sel = np.zeros((S, len(cluster)), np.int32)
+    if len(np.unique(cchroms)) == 1:
+        nc = len(ci(cluster[0]))
+        groups = [[ci(i)[k] for i in cluster] for k in range(nc)]
+        for s in structs:
+            vals = [rg2_f32([crd[b, s] for b in g]) for g in groups]
+            k = int(np.argmin(vals))  # first minimum
+            rg[s], sel[s] = vals[k], groups[k]
+        return rg, sel
+    chroms = list(np.unique(cchroms))
+    by_chrom = [cluster[cchroms == c] for c in chroms]
+    all_segments = np.concatenate(by_chrom)
+    for s in structs:
+        # get_rg2s_cpp on the representatives: mixed-radix combinations, strict <, first found
+        alts = [[crd[b, s] for b in ci(r)] for r in reps]
+        ncomb = int(np.prod([len(a) for a in alts]))
+        best, bestc = f32(1e8), None
+        for k in range(ncomb):
+            kk, comb = k, []
+            for a in alts:
+                comb.append(kk % len(a))
+                kk //= len(a)
+            v = rg2_f32([alts[i][comb[i]] for i in range(len(alts))])
+            if v < best:
+                best, bestc = v, comb
+        choice = {hap_chrom[r]: bestc[i] for i, r in enumerate(reps)}
+        beads = [ci(seg)[choice[hap_chrom[seg]]] for seg in all_segments]
+        rg[s] = rg2_f32([crd[b, s] for b in beads])
+        sel[s] = beads
+    return rg, sel
+
+
+def keep_best(rg2s, k):
+    """argpartition + argsort of SpriteAssignmentStep.task (py:138-139), ties by index."""
+    return np.argsort(rg2s, kind='stable')[:k]
