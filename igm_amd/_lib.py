@@ -35,6 +35,7 @@ IGM_ATOM_ENV0 = 0x10
 # numpy views of the ABI structs (packed exactly like the C layouts)
 pair_dtype = np.dtype([('i', '<i4'), ('j', '<i4'), ('pwish', '<f8'), ('plast', '<f8')])
 row_dtype = np.dtype([('row', '<i4'), ('col', '<i4'), ('dist', '<f4'), ('prob', '<f4')])
+damid_row_dtype = np.dtype([('loc', '<i4'), ('dist', '<f4'), ('prob', '<f4')])
 result_dtype = np.dtype([('ad', '<f8'), ('p', '<f8'), ('pnow', '<f8'), ('o', '<i4'), ('nrows', '<i4')])
 bond_dtype = np.dtype([('i', '<u4'), ('j', '<u4'), ('r0', '<f4'), ('k', '<f4')])
 optinfo_dtype = np.dtype([('final_energy', '<f8'), ('pair_energy', '<f8'), ('bond_energy', '<f8'),
@@ -96,6 +97,12 @@ SIGNATURES = {
     'igm_astep_actdist': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _f64, _i32,
                                  _vp, _vp, _i64, ctypes.POINTER(_i64)]),
     'igm_astep_update_plast': (_i32, [_vp, _u32, _vp, _i64, _vp]),
+    'igm_damid_actdist': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _f64,
+                                 _i32, _vp, _vp, _vp, _i64, ctypes.POINTER(_i64)]),
+    'igm_fish_assign': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp,
+                               _vp, _vp]),
+    'igm_sprite_assign': (_i32, [_vp, _u32, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32,
+                                 _vp, _vp, _vp, _vp]),
     'igm_mstep_run': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp, _vp, _i64,
                              _vp, _vp, _vp, _vp]),
     'igm_mstep_forces': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp, _vp, _i64,

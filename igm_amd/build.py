@@ -29,6 +29,7 @@ SOURCES = {
     'mstep.hip': ['-fno-hip-fp32-correctly-rounded-divide-sqrt'],
     'hic_select.hip': ['-ffp-contract=off'],
     'violations.hip': ['-ffp-contract=off'],
+    'asteps.hip': ['-ffp-contract=off'],
 }
 COMMON = ['-O3', '-fPIC', '-std=c++17', '--offload-arch=%s' % ARCH, '-Wall', '-Wno-unused-function',
           '-munsafe-fp-atomics', '-I%s' % os.path.join(ROOT, 'include')]

@@ -1,0 +1,725 @@
+// A-steps of configurations D/E on the MI355X:
+//
+//   DamID   DamidActivationDistanceStep.task over all loci at once
+//           (igm/steps/DamidActivationDistanceStep.py:223-287, get_damid_actdist_I :376-471)
+//           plus the "%6d %.5f %.5f" text round trip of task()/reduce() (:35, :286, :308).
+//   FISH    FishAssignmentStep.task (igm/steps/FishAssignmentStep.py:188-242):
+//           per-structure min/max radial or pair distance over the copies, ranks,
+//           target[rank] for every probe/pair at once.
+//   SPRITE  SpriteAssignmentStep.task (igm/steps/SpriteAssignmentStep.py:105-160):
+//           compute_gyration_radius (igm/cython_compiled/sprite.pyx:104-283, with
+//           get_rg2s_cpp, cpp_sprite_assignment.cpp:49-143) for every (cluster,
+//           structure), then the keep_best selection (:138-143).
+//
+// All three are HBM/L2-bound gathers over the bead-major (nbead, nstruct, 3) .hss
+// coordinate array; the arithmetic restates NumPy 1.x / the reference C++ operation
+// by operation (no FMA contraction: built with -ffp-contract=off), so the outputs are
+// bit-identical to the reference's.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "exact_math.h"
+#include "igm_ctx.h"
+
+namespace {
+using namespace igm;
+
+constexpr int kBT = 256;  // threads per workgroup (4 waves of 64)
+
+__device__ __forceinline__ int block_sum(int v, int* sh) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    int t = 0;
+    for (int i = 0; i < kBT / 64; ++i) t += sh[i];
+    return t;
+}
+
+__device__ __forceinline__ void load3(const float* __restrict__ xyz, int S, int bead, int s, float& x, float& y,
+                                      float& z) {
+    const float* p = xyz + ((size_t)bead * S + s) * 3;
+    x = p[0];
+    y = p[1];
+    z = p[2];
+}
+
+// ============================================================================ DamID
+struct DamidArgs {
+    const float* xyz;
+    int S;
+    const float* radii;
+    const int* cptr;
+    const int* cidx;
+    const int* loci;
+    const float* pexp;
+    const float* plast;
+    int nloci;
+    int it_corr;
+    int shape;         // 0 sphere, 1 ellipsoid
+    double R[3];       // nucleus_param * (1 - contact_range), f64 (py:436)
+    igm_pair_result* res;
+    const int64_t* rowoff;
+    igm_damid_row* rows;
+};
+
+// snormsq_sphere / snormsq_ellipse (py:39-76): float32 squares, the float64 divisor
+// cast to float32 (NumPy 1.x value-based casting), float32 divisions and sums
+__device__ __forceinline__ float damid_key(const DamidArgs& A, int bead, int s, float D0, float D1, float D2) {
+    float x, y, z;
+    load3(A.xyz, A.S, bead, s, x, y, z);
+    const float q0 = __fmul_rn(x, x), q1 = __fmul_rn(y, y), q2 = __fmul_rn(z, z);
+    if (A.shape == 0) return __fdiv_rn(__fadd_rn(__fadd_rn(q0, q1), q2), D0);
+    return __fadd_rn(__fadd_rn(__fdiv_rn(q0, D0), __fdiv_rn(q1, D1)), __fdiv_rn(q2, D2));
+}
+
+// cleanProbability (DamidActivationDistanceStep.py:362-372) in float64
+__device__ __forceinline__ double damid_clean(double pij, double pexist) {
+    const double pc = (pexist < 1.0) ? (pij - pexist) / (1.0 - pexist) : pij;
+    return pc > 0.0 ? pc : 0.0;
+}
+
+// One workgroup per locus.  The o-th entry of d^2 sorted in decreasing order is the
+// (nS-1-o)-th smallest: found by a 4-pass 8-bit radix select over the float bits
+// (non-negative floats order like their bit patterns; NaN sorts last ascending, first
+// descending, like numpy's sort).  Keys are recomputed from the L2-resident
+// coordinates each pass instead of being staged (nc*S can exceed LDS).
+__global__ void __launch_bounds__(kBT) damid_kernel(DamidArgs A) {
+    const int q = blockIdx.x;
+    if (q >= A.nloci) return;
+    __shared__ int sh_red[kBT / 64];
+    __shared__ unsigned hist[256];
+    __shared__ long long sh_m;
+    __shared__ unsigned sh_prefix, sh_mask;
+    __shared__ double sh_p;
+    __shared__ int sh_o;
+    const int I = A.loci[q];
+    const int c0 = A.cptr[I], nc = A.cptr[I + 1] - c0;
+    const int S = A.S;
+    if (nc <= 0) {
+        if (threadIdx.x == 0) {
+            igm_pair_result r;
+            r.ad = __longlong_as_double(0x7ff8000000000000LL);
+            r.p = 0.0;
+            r.pnow = 0.0;
+            r.o = -1;
+            r.nrows = 0;
+            A.res[q] = r;
+        }
+        return;
+    }
+    const float rad = A.radii[A.cidx[c0]];  // r = radii[ii[0]] (py:429)
+    float D0, D1 = 1.0f, D2 = 1.0f;
+    if (A.shape == 0) {
+        const double t = A.R[0] - (double)rad;
+        D0 = (float)(t * t);
+    } else {
+        const double a = A.R[0] - (double)rad, b = A.R[1] - (double)rad, c = A.R[2] - (double)rad;
+        D0 = (float)(a * a);
+        D1 = (float)(b * b);
+        D2 = (float)(c * c);
+    }
+    // contact count: d_sq >= rcutsq = 1.0 (py:449-450)
+    int cnt = 0;
+    for (int ci = 0; ci < nc; ++ci) {
+        const int bead = A.cidx[c0 + ci];
+        for (int s = threadIdx.x; s < S; s += kBT) cnt += damid_key(A, bead, s, D0, D1, D2) >= 1.0f;
+    }
+    cnt = block_sum(cnt, sh_red);
+    const int64_t nS = (int64_t)nc * S;
+    if (threadIdx.x == 0) {
+        const double pnow = (double)cnt / (double)nS;
+        const double pexp = (double)A.pexp[q];
+        double p;
+        if (A.it_corr == 1) {
+            p = damid_clean(pexp, damid_clean(pnow, (double)A.plast[q]));
+        } else {
+            p = pexp;
+        }
+        int o = -1;
+        if (p > 0.0) {  // o = min(nS - 1, int(round(nS * p)))  (py:464-466, half to even)
+            const double ox = rint((double)nS * p);
+            o = (ox >= (double)(nS - 1)) ? (int)(nS - 1) : (int)ox;
+        }
+        sh_p = p;
+        sh_o = o;
+        sh_m = o >= 0 ? nS - 1 - o : 0;
+        sh_prefix = 0u;
+        sh_mask = 0u;
+        igm_pair_result r;
+        r.p = p;
+        r.pnow = pnow;
+        r.o = o;
+        r.nrows = nc;
+        r.ad = __longlong_as_double(0x7ff8000000000000LL);
+        A.res[q] = r;
+    }
+    __syncthreads();
+    const int o = sh_o;
+    double ad = 2.0;  // py:460
+    if (o >= 0) {
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            hist[threadIdx.x] = 0u;
+            __syncthreads();
+            const unsigned prefix = sh_prefix, mask = sh_mask;
+            for (int ci = 0; ci < nc; ++ci) {
+                const int bead = A.cidx[c0 + ci];
+                for (int s = threadIdx.x; s < S; s += kBT) {
+                    const unsigned u = __float_as_uint(damid_key(A, bead, s, D0, D1, D2));
+                    if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                long long m = sh_m;
+                int b = 0;
+                for (; b < 255; ++b) {
+                    if (m < (long long)hist[b]) break;
+                    m -= hist[b];
+                }
+                sh_m = m;
+                sh_prefix = prefix | ((unsigned)b << shift);
+                sh_mask = mask | (255u << shift);
+            }
+            __syncthreads();
+        }
+        ad = sqrt_rn((double)__uint_as_float(sh_prefix));  // np.sqrt(d_sq[o]) in float64 (py:470)
+        if (threadIdx.x == 0) A.res[q].ad = ad;
+    }
+    // rows (i, ad, p) for i in ii (py:473) through '%.5f' and genfromtxt(float32)
+    const float dist = (float)round_dec(ad, 1e5);
+    const float prob = (float)round_dec(sh_p, 1e5);
+    const int64_t base = A.rowoff[q];
+    for (int ci = threadIdx.x; ci < nc; ci += kBT) {
+        igm_damid_row w;
+        w.loc = A.cidx[c0 + ci];
+        w.dist = dist;
+        w.prob = prob;
+        A.rows[base + ci] = w;
+    }
+}
+
+__global__ void damid_nrows_kernel(const int* __restrict__ loci, int nloci, const int* __restrict__ cptr,
+                                   int64_t* __restrict__ nr) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nloci) nr[q] = cptr[loci[q] + 1] - cptr[loci[q]];
+}
+
+__global__ void check_loci_kernel(const int* __restrict__ loci, int n, int nhap, int* __restrict__ bad) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n && (loci[q] < 0 || loci[q] >= nhap)) atomicOr(bad, 1);
+}
+
+// ============================================================================ FISH
+struct FishArgs {
+    const float* xyz;
+    int S;
+    const int* cptr;
+    const int* cidx;
+    int kind;  // 0 radial (items[q]), 1 pair (items[2q], items[2q+1])
+    const int* items;
+    int nitems;
+    const float* tmin;
+    const float* tmax;
+    float* omin;
+    float* omax;
+    float* dmin;
+    float* dmax;
+};
+
+// np.linalg.norm(x, axis=1) in float32: sqrt(((x0^2 + x1^2) + x2^2)), correctly rounded
+__device__ __forceinline__ float norm3(float x, float y, float z) {
+    return sqrtf_rn(__fadd_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)), __fmul_rn(z, z)));
+}
+
+// One workgroup per probe/pair: the per-structure min and max over the copies
+// (get_rad_dists / get_pair_dists + get_min_max_and_idx, py:23-77) are staged in
+// LDS, then every structure's rank -- argsort(argsort(.)), ties in index order -- is
+// counted against the whole column, and target[rank] is written (py:221-242).
+__global__ void __launch_bounds__(kBT) fish_kernel(FishArgs A) {
+    extern __shared__ float fsm[];
+    const int q = blockIdx.x;
+    if (q >= A.nitems) return;
+    const int S = A.S;
+    float* vmin = fsm;
+    float* vmax = fsm + S;
+    int a0, na, b0 = 0, nb = 0;
+    if (A.kind == 0) {
+        const int h = A.items[q];
+        a0 = A.cptr[h];
+        na = A.cptr[h + 1] - a0;
+    } else {
+        const int h = A.items[2 * q], g = A.items[2 * q + 1];
+        a0 = A.cptr[h];
+        na = A.cptr[h + 1] - a0;
+        b0 = A.cptr[g];
+        nb = A.cptr[g + 1] - b0;
+    }
+    for (int s = threadIdx.x; s < S; s += kBT) {
+        float mn = INFINITY, mx = -INFINITY;
+        for (int a = 0; a < na; ++a) {
+            float x, y, z;
+            load3(A.xyz, S, A.cidx[a0 + a], s, x, y, z);
+            if (A.kind == 0) {
+                const float d = norm3(x, y, z);
+                mn = d < mn ? d : mn;
+                mx = d > mx ? d : mx;
+            } else {
+                for (int b = 0; b < nb; ++b) {
+                    float u, v, w;
+                    load3(A.xyz, S, A.cidx[b0 + b], s, u, v, w);
+                    const float d = norm3(__fsub_rn(x, u), __fsub_rn(y, v), __fsub_rn(z, w));
+                    mn = d < mn ? d : mn;
+                    mx = d > mx ? d : mx;
+                }
+            }
+        }
+        vmin[s] = mn;
+        vmax[s] = mx;
+    }
+    __syncthreads();
+    const size_t row = (size_t)q * S;
+    for (int s = threadIdx.x; s < S; s += kBT) {
+        const float mn = vmin[s], mx = vmax[s];
+        int rmin = 0, rmax = 0;
+        int t = 0;
+        for (; t + 4 <= S; t += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float a = vmin[t + u], b = vmax[t + u];
+                rmin += (a < mn) | ((a == mn) & (t + u < s));
+                rmax += (b < mx) | ((b == mx) & (t + u < s));
+            }
+        }
+        for (; t < S; ++t) {
+            const float a = vmin[t], b = vmax[t];
+            rmin += (a < mn) | ((a == mn) & (t < s));
+            rmax += (b < mx) | ((b == mx) & (t < s));
+        }
+        if (A.omin) A.omin[row + s] = A.tmin[row + rmin];
+        if (A.omax) A.omax[row + s] = A.tmax[row + rmax];
+        if (A.dmin) A.dmin[row + s] = mn;
+        if (A.dmax) A.dmax[row + s] = mx;
+    }
+}
+
+// ============================================================================ SPRITE
+struct SpriteArgs {
+    const float* xyz;
+    int S;
+    int ncl;
+    int nsb;  // structure blocks per cluster
+    const int* seg_ptr;
+    const int* seg_region;
+    const int* seg_rep;
+    const int* rep_ptr;
+    const int* rep_region;
+    const int* alt_ptr;
+    const int* alt_bead;
+    float* rg2;  // (ncl, S)
+    int* sel;    // (nseg, S): the selected bead of every cluster segment
+};
+
+constexpr float kSpriteInf = 100000000.0f;  // INF of cpp_sprite_assignment.cpp:4
+constexpr int kMaxReps = 16;
+
+// gyration_radius_sq (cpp_sprite_assignment.cpp:49-61): float mean accumulated in
+// order and divided by float(n), then the sum of X0*X0 + X1*X1 + X2*X2 in order / n
+template <class Bead>
+__device__ __forceinline__ float rg2_of(const float* __restrict__ xyz, int S, int s, int n, Bead bead) {
+    float mx = 0.0f, my = 0.0f, mz = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        float x, y, z;
+        load3(xyz, S, bead(i), s, x, y, z);
+        mx = __fadd_rn(mx, x);
+        my = __fadd_rn(my, y);
+        mz = __fadd_rn(mz, z);
+    }
+    const float fn = (float)n;
+    mx = __fdiv_rn(mx, fn);
+    my = __fdiv_rn(my, fn);
+    mz = __fdiv_rn(mz, fn);
+    float rg = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        float x, y, z;
+        load3(xyz, S, bead(i), s, x, y, z);
+        const float dx = __fsub_rn(x, mx), dy = __fsub_rn(y, my), dz = __fsub_rn(z, mz);
+        rg = __fadd_rn(rg, __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+    }
+    return __fdiv_rn(rg, fn);
+}
+
+// Python indexing of a copy list by the selected copy: -1 (no combination below INF)
+// wraps to the last copy, as curr_beads[sel] does in sprite.pyx:268
+__device__ __forceinline__ int alt_of(const SpriteArgs& A, int region, int k) {
+    const int a0 = A.alt_ptr[region], n = A.alt_ptr[region + 1] - a0;
+    return A.alt_bead[a0 + (k < 0 ? n + k : k)];
+}
+
+// One thread per (cluster, structure), consecutive structures across the wave so the
+// coordinate gathers of a bead are contiguous.
+//  single-chromosome clusters (no representatives): every copy k of the segments is a
+//    group; the group with the smallest Rg^2 (first on ties, sprite.pyx:184-200) wins;
+//  multi-chromosome clusters: get_rg2s_cpp over the representatives' copy
+//    combinations (mixed radix, first representative fastest; strict <, first found),
+//    then Rg^2 of all segments with each chromosome's selected copy (sprite.pyx:231-283).
+// Every Rg^2 goes through get_rg2s_cpp in the reference, so a value not below INF
+// reads as INF.
+__global__ void __launch_bounds__(kBT) sprite_rg2_kernel(SpriteArgs A) {
+    const int c = blockIdx.x / A.nsb;
+    const int s = (blockIdx.x - c * A.nsb) * kBT + threadIdx.x;
+    if (c >= A.ncl || s >= A.S) return;
+    const int g0 = A.seg_ptr[c], ng = A.seg_ptr[c + 1] - g0;
+    const int r0 = A.rep_ptr[c], nr = A.rep_ptr[c + 1] - r0;
+    const int S = A.S;
+    float best;
+    if (nr == 0) {
+        const int nalt = A.alt_ptr[A.seg_region[g0] + 1] - A.alt_ptr[A.seg_region[g0]];
+        best = kSpriteInf;
+        int bk = 0;
+        for (int k = 0; k < nalt; ++k) {
+            float v = rg2_of(A.xyz, S, s, ng, [&](int i) { return alt_of(A, A.seg_region[g0 + i], k); });
+            v = v < kSpriteInf ? v : kSpriteInf;
+            if (k == 0 || v < best) {
+                best = v;
+                bk = k;
+            }
+        }
+        for (int i = 0; i < ng; ++i) A.sel[(size_t)(g0 + i) * S + s] = alt_of(A, A.seg_region[g0 + i], bk);
+    } else {
+        int ncomb = 1;
+        int nalt[kMaxReps];
+        for (int i = 0; i < nr; ++i) {
+            const int rg = A.rep_region[r0 + i];
+            nalt[i] = A.alt_ptr[rg + 1] - A.alt_ptr[rg];
+            ncomb *= nalt[i];
+        }
+        float bv = kSpriteInf;
+        int bcomb = -1;
+        for (int k = 0; k < ncomb; ++k) {
+            const float v = rg2_of(A.xyz, S, s, nr, [&](int i) {
+                int kk = k, ci = 0;
+                for (int j = 0; j <= i; ++j) {
+                    ci = kk % nalt[j];
+                    kk /= nalt[j];
+                }
+                return alt_of(A, A.rep_region[r0 + i], ci);
+            });
+            if (v < bv) {
+                bv = v;
+                bcomb = k;
+            }
+        }
+        // the chosen copy of representative i (-1 when no combination was below INF)
+        auto choice = [&](int i) {
+            if (bcomb < 0) return -1;
+            int kk = bcomb, ci = 0;
+            for (int j = 0; j <= i; ++j) {
+                ci = kk % nalt[j];
+                kk /= nalt[j];
+            }
+            return ci;
+        };
+        for (int i = 0; i < ng; ++i)
+            A.sel[(size_t)(g0 + i) * S + s] = alt_of(A, A.seg_region[g0 + i], choice(A.seg_rep[g0 + i]));
+        best = rg2_of(A.xyz, S, s, ng, [&](int i) { return A.sel[(size_t)(g0 + i) * S + s]; });
+        best = best < kSpriteInf ? best : kSpriteInf;
+    }
+    A.rg2[(size_t)c * S + s] = best;
+}
+
+// keep_best (SpriteAssignmentStep.py:138-143): the keep_best smallest Rg^2 of a
+// cluster in increasing order (ties by structure index), their values and the
+// selected beads of those structures, row-major (keep_best, len(cluster)).
+__global__ void __launch_bounds__(kBT) sprite_keep_best_kernel(const float* __restrict__ rg2, const int* __restrict__ sel,
+                                                               const int* __restrict__ seg_ptr, int S, int kb,
+                                                               int* __restrict__ best_idx, float* __restrict__ best_val,
+                                                               int* __restrict__ best_sel) {
+    extern __shared__ float ksm[];
+    const int c = blockIdx.x;
+    const float* v = rg2 + (size_t)c * S;
+    for (int s = threadIdx.x; s < S; s += kBT) ksm[s] = v[s];
+    __syncthreads();
+    const int g0 = seg_ptr[c], ng = seg_ptr[c + 1] - g0;
+    for (int s = threadIdx.x; s < S; s += kBT) {
+        const float x = ksm[s];
+        int r = 0;
+        for (int t = 0; t < S && r < kb; ++t) {
+            const float y = ksm[t];
+            r += (y < x) | ((y == x) & (t < s));
+        }
+        if (r < kb) {
+            best_idx[(size_t)c * kb + r] = s;
+            best_val[(size_t)c * kb + r] = x;
+            int* out = best_sel + (size_t)g0 * kb + (size_t)r * ng;
+            for (int i = 0; i < ng; ++i) out[i] = sel[(size_t)(g0 + i) * S + s];
+        }
+    }
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" int igm_damid_actdist(igm_ctx* c, uint32_t flags, const float* xyz, int32_t nbead, int32_t nstruct,
+                                 const float* radii, const int32_t* copy_ptr, const int32_t* copy_idx, int32_t nhap,
+                                 const int32_t* loci, const float* p_exp, const float* plast, int32_t nloci,
+                                 int32_t it_corr, double contact_range, int32_t shape, const double* nucleus_param,
+                                 igm_pair_result* per_locus, igm_damid_row* rows, int64_t row_capacity,
+                                 int64_t* nrows_out) {
+    if (!c) return IGM_E_INVALID;
+    if (nbead <= 0 || nstruct <= 0 || nhap <= 0 || nloci < 0 || !xyz || !radii || !copy_ptr || !copy_idx ||
+        (nloci > 0 && (!loci || !p_exp || !plast)) || !nrows_out || !nucleus_param || (shape != 0 && shape != 1))
+        return fail(c, IGM_E_INVALID, "igm_damid_actdist: invalid arguments");
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    *nrows_out = 0;
+    if (nloci == 0) return IGM_OK;
+    int32_t ncopy = 0;
+    if (flags & IGM_DEVICE_PTRS) {
+        IGM_HIP_CHECK(c, hipMemcpyAsync(&ncopy, copy_ptr + nhap, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    } else {
+        ncopy = copy_ptr[nhap];
+    }
+    const float *d_xyz, *d_radii, *d_pexp, *d_plast;
+    const int32_t *d_cptr, *d_cidx, *d_loci;
+    IGM_TRY(to_device(c, flags, "dm_xyz", xyz, (size_t)nbead * nstruct * 3, &d_xyz));
+    IGM_TRY(to_device(c, flags, "dm_radii", radii, (size_t)nbead, &d_radii));
+    IGM_TRY(to_device(c, flags, "dm_cptr", copy_ptr, (size_t)nhap + 1, &d_cptr));
+    IGM_TRY(to_device(c, flags, "dm_cidx", copy_idx, (size_t)ncopy, &d_cidx));
+    IGM_TRY(to_device(c, flags, "dm_loci", loci, (size_t)nloci, &d_loci));
+    IGM_TRY(to_device(c, flags, "dm_pexp", p_exp, (size_t)nloci, &d_pexp));
+    IGM_TRY(to_device(c, flags, "dm_plast", plast, (size_t)nloci, &d_plast));
+    void *p_bad, *p_nr, *p_off;
+    IGM_TRY(workspace(c, "dm_bad", sizeof(int), &p_bad));
+    IGM_TRY(workspace(c, "dm_nr", (size_t)nloci * sizeof(int64_t), &p_nr));
+    IGM_TRY(workspace(c, "dm_off", (size_t)nloci * sizeof(int64_t), &p_off));
+    const unsigned g1 = (unsigned)ceil_div(nloci, 256);
+    IGM_HIP_CHECK(c, hipMemsetAsync(p_bad, 0, sizeof(int), c->stream));
+    hipLaunchKernelGGL(check_loci_kernel, dim3(g1), dim3(256), 0, c->stream, d_loci, nloci, nhap, (int*)p_bad);
+    IGM_HIP_CHECK(c, hipGetLastError());
+    int bad = 0;
+    IGM_HIP_CHECK(c, hipMemcpyAsync(&bad, p_bad, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    if (bad) return fail(c, IGM_E_INVALID, "igm_damid_actdist: locus index outside [0, %d)", nhap);
+    int64_t* d_nr = (int64_t*)p_nr;
+    int64_t* d_off = (int64_t*)p_off;
+    hipLaunchKernelGGL(damid_nrows_kernel, dim3(g1), dim3(256), 0, c->stream, d_loci, nloci, d_cptr, d_nr);
+    IGM_HIP_CHECK(c, hipGetLastError());
+    size_t tmp_bytes = 0;
+    IGM_HIP_CHECK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_nr, d_off, (int)nloci, c->stream));
+    void* d_tmp;
+    IGM_TRY(workspace(c, "dm_scan_tmp", tmp_bytes, &d_tmp));
+    IGM_HIP_CHECK(c, hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_nr, d_off, (int)nloci, c->stream));
+    int64_t last_off = 0, last_n = 0;
+    IGM_HIP_CHECK(c, hipMemcpyAsync(&last_off, d_off + nloci - 1, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    IGM_HIP_CHECK(c, hipMemcpyAsync(&last_n, d_nr + nloci - 1, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    const int64_t total = last_off + last_n;
+    *nrows_out = total;
+    if (total > row_capacity || (total > 0 && !rows))
+        return fail(c, IGM_E_OVERFLOW, "igm_damid_actdist: %lld rows exceed capacity %lld", (long long)total,
+                    (long long)row_capacity);
+    igm_pair_result* d_res;
+    if (per_locus && (flags & IGM_DEVICE_PTRS)) {
+        d_res = per_locus;
+    } else {
+        void* p;
+        IGM_TRY(workspace(c, "dm_res", (size_t)nloci * sizeof(igm_pair_result), &p));
+        d_res = (igm_pair_result*)p;
+    }
+    igm_damid_row* d_rows;
+    IGM_TRY(out_device(c, flags, "dm_rows", rows, (size_t)total, &d_rows));
+    DamidArgs A;
+    A.xyz = d_xyz;
+    A.S = nstruct;
+    A.radii = d_radii;
+    A.cptr = d_cptr;
+    A.cidx = d_cidx;
+    A.loci = d_loci;
+    A.pexp = d_pexp;
+    A.plast = d_plast;
+    A.nloci = nloci;
+    A.it_corr = it_corr;
+    A.shape = shape;
+    for (int k = 0; k < 3; ++k) A.R[k] = nucleus_param[shape == 0 ? 0 : k] * (1.0 - contact_range);
+    A.res = d_res;
+    A.rowoff = d_off;
+    A.rows = d_rows;
+    {
+        Timed tm(c, "damid");
+        hipLaunchKernelGGL(damid_kernel, dim3((unsigned)nloci), dim3(kBT), 0, c->stream, A);
+        IGM_HIP_CHECK(c, hipGetLastError());
+    }
+    IGM_TRY(to_host(c, flags, rows, d_rows, (size_t)total));
+    if (per_locus && !(flags & IGM_DEVICE_PTRS)) IGM_TRY(to_host(c, flags, per_locus, d_res, (size_t)nloci));
+    return finish(c, flags);
+}
+
+extern "C" int igm_fish_assign(igm_ctx* c, uint32_t flags, const float* xyz, int32_t nbead, int32_t nstruct,
+                               const int32_t* copy_ptr, const int32_t* copy_idx, int32_t nhap, int32_t kind,
+                               const int32_t* items, int32_t nitems, const float* target_min,
+                               const float* target_max, float* out_min, float* out_max, float* dist_min,
+                               float* dist_max) {
+    if (!c) return IGM_E_INVALID;
+    if (nbead <= 0 || nstruct <= 0 || nhap <= 0 || nitems < 0 || !xyz || !copy_ptr || !copy_idx ||
+        (kind != 0 && kind != 1) || (nitems > 0 && !items) || (out_min && !target_min) || (out_max && !target_max))
+        return fail(c, IGM_E_INVALID, "igm_fish_assign: invalid arguments");
+    const size_t lds = (size_t)2 * nstruct * sizeof(float);
+    if (lds > (size_t)160 * 1024 - 1024)
+        return fail(c, IGM_E_UNSUPPORTED, "igm_fish_assign: %d structures exceed the LDS-resident rank kernel",
+                    nstruct);
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    if (nitems == 0) return IGM_OK;
+    int32_t ncopy = 0;
+    if (flags & IGM_DEVICE_PTRS) {
+        IGM_HIP_CHECK(c, hipMemcpyAsync(&ncopy, copy_ptr + nhap, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    } else {
+        ncopy = copy_ptr[nhap];
+        const int per = kind == 0 ? 1 : 2;
+        for (int64_t k = 0; k < (int64_t)nitems * per; ++k)
+            if (items[k] < 0 || items[k] >= nhap)
+                return fail(c, IGM_E_INVALID, "igm_fish_assign: item locus %d outside [0, %d)", items[k], nhap);
+    }
+    const float *d_xyz, *d_tmin, *d_tmax;
+    const int32_t *d_cptr, *d_cidx, *d_items;
+    const size_t nout = (size_t)nitems * nstruct;
+    IGM_TRY(to_device(c, flags, "fi_xyz", xyz, (size_t)nbead * nstruct * 3, &d_xyz));
+    IGM_TRY(to_device(c, flags, "fi_cptr", copy_ptr, (size_t)nhap + 1, &d_cptr));
+    IGM_TRY(to_device(c, flags, "fi_cidx", copy_idx, (size_t)ncopy, &d_cidx));
+    IGM_TRY(to_device(c, flags, "fi_items", items, (size_t)nitems * (kind == 0 ? 1 : 2), &d_items));
+    IGM_TRY(to_device(c, flags, "fi_tmin", out_min ? target_min : nullptr, nout, &d_tmin));
+    IGM_TRY(to_device(c, flags, "fi_tmax", out_max ? target_max : nullptr, nout, &d_tmax));
+    float *d_omin, *d_omax, *d_dmin, *d_dmax;
+    IGM_TRY(out_device(c, flags, "fi_omin", out_min, nout, &d_omin));
+    IGM_TRY(out_device(c, flags, "fi_omax", out_max, nout, &d_omax));
+    IGM_TRY(out_device(c, flags, "fi_dmin", dist_min, nout, &d_dmin));
+    IGM_TRY(out_device(c, flags, "fi_dmax", dist_max, nout, &d_dmax));
+    if (lds > 65536) IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)fish_kernel,
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    FishArgs A{d_xyz, nstruct, d_cptr, d_cidx, kind, d_items, nitems, d_tmin, d_tmax, d_omin, d_omax, d_dmin, d_dmax};
+    {
+        Timed tm(c, "fish");
+        hipLaunchKernelGGL(fish_kernel, dim3((unsigned)nitems), dim3(kBT), lds, c->stream, A);
+        IGM_HIP_CHECK(c, hipGetLastError());
+    }
+    IGM_TRY(to_host(c, flags, out_min, d_omin, nout));
+    IGM_TRY(to_host(c, flags, out_max, d_omax, nout));
+    IGM_TRY(to_host(c, flags, dist_min, d_dmin, nout));
+    IGM_TRY(to_host(c, flags, dist_max, d_dmax, nout));
+    return finish(c, flags);
+}
+
+extern "C" int igm_sprite_assign(igm_ctx* c, uint32_t flags, const float* xyz, int32_t nbead, int32_t nstruct,
+                                 int32_t ncluster, const int32_t* seg_ptr, const int32_t* seg_region,
+                                 const int32_t* seg_rep, const int32_t* rep_ptr, const int32_t* rep_region,
+                                 int32_t nregion, const int32_t* alt_ptr, const int32_t* alt_bead, int32_t keep_best,
+                                 float* rg2_out, int32_t* best_idx, float* best_rg2, int32_t* best_sel) {
+    if (!c) return IGM_E_INVALID;
+    if (nbead <= 0 || nstruct <= 0 || ncluster < 0 || nregion < 0 || !xyz || !seg_ptr || !rep_ptr || !alt_ptr ||
+        keep_best < 0 || (keep_best > 0 && (!best_idx || !best_rg2 || !best_sel)))
+        return fail(c, IGM_E_INVALID, "igm_sprite_assign: invalid arguments");
+    if (keep_best >= nstruct && keep_best > 0)
+        return fail(c, IGM_E_INVALID, "igm_sprite_assign: keep_best %d must be < nstruct %d (np.argpartition)",
+                    keep_best, nstruct);
+    if ((size_t)nstruct * sizeof(float) > (size_t)64 * 1024)
+        return fail(c, IGM_E_UNSUPPORTED, "igm_sprite_assign: %d structures exceed the LDS-resident selection",
+                    nstruct);
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    if (ncluster == 0) return IGM_OK;
+    if (flags & IGM_DEVICE_PTRS)
+        return fail(c, IGM_E_UNSUPPORTED, "igm_sprite_assign: host CSR arrays expected (validated on the host)");
+    // host validation of the CSR description (the kernels trust it)
+    const int nseg = seg_ptr[ncluster], nrep = rep_ptr[ncluster], nalt = alt_ptr[nregion];
+    if (seg_ptr[0] != 0 || rep_ptr[0] != 0 || alt_ptr[0] != 0 || nseg < 0 || nrep < 0 || nalt < 0 ||
+        (nseg > 0 && (!seg_region || !seg_rep)) || (nrep > 0 && !rep_region) || (nalt > 0 && !alt_bead))
+        return fail(c, IGM_E_INVALID, "igm_sprite_assign: malformed CSR arrays");
+    for (int r = 0; r < nregion; ++r)
+        if (alt_ptr[r + 1] <= alt_ptr[r]) return fail(c, IGM_E_INVALID, "igm_sprite_assign: region %d has no copies", r);
+    for (int k = 0; k < nalt; ++k)
+        if (alt_bead[k] < 0 || alt_bead[k] >= nbead)
+            return fail(c, IGM_E_INVALID, "igm_sprite_assign: bead %d outside [0, %d)", alt_bead[k], nbead);
+    for (int q = 0; q < ncluster; ++q) {
+        const int g0 = seg_ptr[q], ng = seg_ptr[q + 1] - g0, r0 = rep_ptr[q], nr = rep_ptr[q + 1] - r0;
+        if (ng <= 0 || nr < 0 || nr > kMaxReps)
+            return fail(c, IGM_E_INVALID, "igm_sprite_assign: cluster %d has %d segments, %d representatives", q, ng,
+                        nr);
+        long long ncomb = 1;
+        for (int i = 0; i < nr; ++i) {
+            const int rg = rep_region[r0 + i];
+            if (rg < 0 || rg >= nregion) return fail(c, IGM_E_INVALID, "igm_sprite_assign: bad region id");
+            ncomb *= alt_ptr[rg + 1] - alt_ptr[rg];
+            if (ncomb > (1 << 20)) return fail(c, IGM_E_UNSUPPORTED, "igm_sprite_assign: too many copy combinations");
+        }
+        int nalt0 = -1;
+        for (int i = 0; i < ng; ++i) {
+            const int rg = seg_region[g0 + i];
+            if (rg < 0 || rg >= nregion) return fail(c, IGM_E_INVALID, "igm_sprite_assign: bad region id");
+            const int na = alt_ptr[rg + 1] - alt_ptr[rg];
+            if (nr == 0) {
+                if (nalt0 >= 0 && na < nalt0)
+                    return fail(c, IGM_E_INVALID, "igm_sprite_assign: cluster %d segments differ in copy count", q);
+                if (nalt0 < 0) nalt0 = na;
+            } else {
+                const int rp = seg_rep[g0 + i];
+                if (rp < 0 || rp >= nr) return fail(c, IGM_E_INVALID, "igm_sprite_assign: bad representative slot");
+                if (alt_ptr[rep_region[r0 + rp] + 1] - alt_ptr[rep_region[r0 + rp]] > na)
+                    return fail(c, IGM_E_INVALID, "igm_sprite_assign: segment has fewer copies than its chromosome");
+            }
+        }
+    }
+    const float* d_xyz;
+    const int32_t *d_sp, *d_sr, *d_srep, *d_rp, *d_rr, *d_ap, *d_ab;
+    IGM_TRY(to_device(c, flags, "sp_xyz", xyz, (size_t)nbead * nstruct * 3, &d_xyz));
+    IGM_TRY(to_device(c, flags, "sp_sp", seg_ptr, (size_t)ncluster + 1, &d_sp));
+    IGM_TRY(to_device(c, flags, "sp_sr", seg_region, (size_t)nseg, &d_sr));
+    IGM_TRY(to_device(c, flags, "sp_srep", seg_rep, (size_t)nseg, &d_srep));
+    IGM_TRY(to_device(c, flags, "sp_rp", rep_ptr, (size_t)ncluster + 1, &d_rp));
+    IGM_TRY(to_device(c, flags, "sp_rr", rep_region, (size_t)nrep, &d_rr));
+    IGM_TRY(to_device(c, flags, "sp_ap", alt_ptr, (size_t)nregion + 1, &d_ap));
+    IGM_TRY(to_device(c, flags, "sp_ab", alt_bead, (size_t)nalt, &d_ab));
+    void *p_rg, *p_sel;
+    IGM_TRY(workspace(c, "sp_rg2", (size_t)ncluster * nstruct * sizeof(float), &p_rg));
+    IGM_TRY(workspace(c, "sp_sel", (size_t)nseg * nstruct * sizeof(int32_t), &p_sel));
+    SpriteArgs A;
+    A.xyz = d_xyz;
+    A.S = nstruct;
+    A.ncl = ncluster;
+    A.nsb = (int)ceil_div(nstruct, kBT);
+    A.seg_ptr = d_sp;
+    A.seg_region = d_sr;
+    A.seg_rep = d_srep;
+    A.rep_ptr = d_rp;
+    A.rep_region = d_rr;
+    A.alt_ptr = d_ap;
+    A.alt_bead = d_ab;
+    A.rg2 = (float*)p_rg;
+    A.sel = (int*)p_sel;
+    if ((int64_t)ncluster * A.nsb > 0x7fffffff) return fail(c, IGM_E_UNSUPPORTED, "igm_sprite_assign: grid too large");
+    int32_t *d_bi = nullptr, *d_bs = nullptr;
+    float* d_bv = nullptr;
+    const size_t nb = (size_t)ncluster * keep_best, nbs = (size_t)nseg * keep_best;
+    IGM_TRY(out_device(c, flags, "sp_bi", best_idx, nb, &d_bi));
+    IGM_TRY(out_device(c, flags, "sp_bv", best_rg2, nb, &d_bv));
+    IGM_TRY(out_device(c, flags, "sp_bs", best_sel, nbs, &d_bs));
+    {
+        Timed tm(c, "sprite");
+        hipLaunchKernelGGL(sprite_rg2_kernel, dim3((unsigned)(ncluster * A.nsb)), dim3(kBT), 0, c->stream, A);
+        IGM_HIP_CHECK(c, hipGetLastError());
+        if (keep_best > 0) {
+            hipLaunchKernelGGL(sprite_keep_best_kernel, dim3((unsigned)ncluster), dim3(kBT),
+                               (size_t)nstruct * sizeof(float), c->stream, (const float*)p_rg, (const int*)p_sel, d_sp,
+                               nstruct, keep_best, d_bi, d_bv, d_bs);
+            IGM_HIP_CHECK(c, hipGetLastError());
+        }
+    }
+    IGM_TRY(to_host(c, flags, rg2_out, (const float*)p_rg, (size_t)ncluster * nstruct));
+    if (keep_best > 0) {
+        IGM_TRY(to_host(c, flags, best_idx, d_bi, nb));
+        IGM_TRY(to_host(c, flags, best_rg2, d_bv, nb));
+        IGM_TRY(to_host(c, flags, best_sel, d_bs, nbs));
+    }
+    return finish(c, flags);
+}

@@ -29,4 +29,27 @@ __device__ __forceinline__ bool sqrt_le(float d2, float dist) {
     return (double)d2 < m * m;  // m has <= 25 significant bits: m*m is exact
 }
 
+// float('%.Nf' % x) with scale = 10^N (N <= 15): CPython formats the exact binary
+// value rounded half-to-even to N decimals, and float() returns the double nearest
+// that decimal, i.e. RN(k / 10^N).  x*scale is split exactly into hi + lo.
+__device__ __forceinline__ double round_dec(double x, double scale) {
+    if (!isfinite(x)) return x;
+    const double hi = x * scale;
+    const double lo = fma(x, scale, -hi);
+    double r = rint(hi);
+    const double t = hi - r;  // exact
+    const double u = (t - 0.5) + lo;
+    const double w = (t + 0.5) + lo;
+    if (u > 0.0) {
+        r += 1.0;
+    } else if (u == 0.0) {
+        if (fmod(r, 2.0) != 0.0) r += 1.0;
+    } else if (w < 0.0) {
+        r -= 1.0;
+    } else if (w == 0.0) {
+        if (fmod(r, 2.0) != 0.0) r -= 1.0;
+    }
+    return r / scale;
+}
+
 }  // namespace igm

@@ -157,3 +157,57 @@ def hic_pairs_200kb(sigma, max_sep=200, inter_density=1e-4, seed=0):
     m = p >= sigma
     order = np.lexsort((j[m], i[m]))
     return i[m][order], j[m][order], p[m][order]
+
+
+# ---- configurations D/E A-step inputs ----------------------
+ELLIPSOID_D = (7840.0, 6470.0, 2450.0)
+
+
+def damid_profile_200kb(seed=1):
+    """Config D: DamID lamina-contact profile over the 15 453 haploid 200 kb loci,
+    p ~ Beta(2, 5) with rng(seed), float32 (the reference loads it as float32 text)."""
+    nhap = male_diploid_index(200000)['nhap']
+    return np.random.default_rng(seed).beta(2.0, 5.0, nhap).astype(np.float32)
+
+
+def sprite_clusters_200kb(nclusters=100000, seed=2, lo=2, hi=20):
+    """Config E: SPRITE clusters of lo..hi haploid loci.  Half are runs on one
+    chromosome, half draw from 2..6 chromosomes (each a short run) -- the mix of
+    single- and multi-chromosome clusters the reference handles.  Returns
+    (indptr, data) like the clusters h5 (SpriteAssignmentStep.py:84-99)."""
+    ix = male_diploid_index(200000)
+    hc = ix['hap_chrom']
+    starts = np.concatenate([[0], np.cumsum(np.bincount(hc))])
+    rng = np.random.default_rng(seed)
+    ptr, data = [0], []
+    for c in range(nclusters):
+        n = int(rng.integers(lo, hi + 1))
+        nch = 1 if c % 2 == 0 else int(rng.integers(2, 7))
+        chroms = rng.choice(24, size=nch, replace=False)
+        parts = np.array_split(np.arange(n), nch)
+        cl = []
+        for ch, part in zip(chroms, parts):
+            if len(part) == 0:
+                continue
+            size = starts[ch + 1] - starts[ch]
+            st = int(rng.integers(0, size - len(part)))
+            cl.extend(range(starts[ch] + st, starts[ch] + st + len(part)))
+        cl = np.unique(cl)
+        data.extend(cl.tolist())
+        ptr.append(len(data))
+    return np.asarray(ptr, np.int64), np.asarray(data, np.int32)
+
+
+def fish_inputs_200kb(nstruct, nprobe=500, npair=500, seed=3):
+    """Config E: FISH probes and pairs over the 200 kb loci with sorted LogNormal
+    target distributions x S (nm)."""
+    nhap = male_diploid_index(200000)['nhap']
+    rng = np.random.default_rng(seed)
+    probes = np.sort(rng.choice(nhap, nprobe, replace=False)).astype(np.int32)
+    pi = rng.choice(nhap, npair)
+    pj = rng.choice(nhap, npair)
+    pj = np.where(pj == pi, (pj + 1) % nhap, pj)
+    pairs = np.stack([pi, pj], 1).astype(np.int32)
+    srt = lambda m, s, n: np.sort(rng.lognormal(m, s, (n, nstruct)), axis=1).astype(np.float32)
+    return {'probes': probes, 'radial_min': srt(7.5, 0.4, nprobe), 'radial_max': srt(8.0, 0.3, nprobe),
+            'pairs': pairs, 'pair_min': srt(7.0, 0.5, npair), 'pair_max': srt(7.6, 0.4, npair)}

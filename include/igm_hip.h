@@ -100,6 +100,67 @@ int igm_astep_actdist(igm_ctx* ctx, uint32_t flags,
 int igm_astep_update_plast(igm_ctx* ctx, uint32_t flags, igm_pair* pairs, int64_t npairs,
                            const igm_pair_result* per_pair);
 
+/* ---- A-steps of configurations D/E ------------------------------------------
+ * DamID: DamidActivationDistanceStep.task over ALL selected loci in one call
+ * (igm/steps/DamidActivationDistanceStep.py:223-287; get_damid_actdist_I :376-471),
+ * shapes 'sphere' (shape 0, nucleus_param[0] = radius) and 'ellipsoid' (shape 1,
+ * nucleus_param[0..2] = semiaxes), followed by the "%6d %.5f %.5f" text round trip
+ * of task()/reduce() (:35, :286, :308): rows are bit-exact
+ * {i, float32(float('%.5f' % ad)), float32(float('%.5f' % p))} for every copy i of
+ * every locus, in locus order.  loci[q] is a haploid locus, p_exp[q]/plast[q] the
+ * float32 values setup() stores (:199-217).  per_locus[q] (nullable) reports ad, p,
+ * pnow, o (-1 when p <= 0: the dist is then 2) and nrows. */
+typedef struct {
+    int32_t loc; /* diploid bead index                               */
+    float dist;  /* damid_actdist.hdf5 {loc i4, dist f4, prob f4}    */
+    float prob;
+} igm_damid_row;
+
+int igm_damid_actdist(igm_ctx* ctx, uint32_t flags,
+                      const float* xyz, int32_t nbead, int32_t nstruct, /* bead-major (nbead, nstruct, 3) */
+                      const float* radii,
+                      const int32_t* copy_ptr, const int32_t* copy_idx, int32_t nhap,
+                      const int32_t* loci, const float* p_exp, const float* plast, int32_t nloci,
+                      int32_t it_corr, double contact_range, int32_t shape, const double* nucleus_param,
+                      igm_pair_result* per_locus,                  /* (nloci) or NULL */
+                      igm_damid_row* rows, int64_t row_capacity,
+                      int64_t* nrows_out);                         /* host pointer    */
+
+/* FISH: FishAssignmentStep.task (igm/steps/FishAssignmentStep.py:188-242) for all
+ * items at once.  kind 0: items = probes (haploid loci), per structure the min and
+ * max over the copies of |x| (get_rad_dists, :44-58); kind 1: items = (i, j) pairs,
+ * min/max over every copy pair of |x_a - x_b| (get_pair_dists' documented intent,
+ * :23-41).  Distances are float32 np.linalg.norm values.  Each structure's rank
+ * r = argsort(argsort(d)) (:60-77; ties in structure order) selects the target:
+ * out[q, s] = target[q, r].  target_* / out_* / dist_* are (nitems, nstruct) f32;
+ * every output pointer may be NULL (then its target may be NULL too). */
+int igm_fish_assign(igm_ctx* ctx, uint32_t flags,
+                    const float* xyz, int32_t nbead, int32_t nstruct,
+                    const int32_t* copy_ptr, const int32_t* copy_idx, int32_t nhap,
+                    int32_t kind, const int32_t* items, int32_t nitems,
+                    const float* target_min, const float* target_max,
+                    float* out_min, float* out_max, float* dist_min, float* dist_max);
+
+/* SPRITE: SpriteAssignmentStep.task (igm/steps/SpriteAssignmentStep.py:105-160):
+ * compute_gyration_radius (igm/cython_compiled/sprite.pyx:104-283, get_rg2s_cpp
+ * cpp_sprite_assignment.cpp:49-143) for every (cluster, structure), then keep_best.
+ * A "region" is a haploid segment with its copies alt_bead[alt_ptr[r]..alt_ptr[r+1]).
+ * Cluster c has the segments seg_region[seg_ptr[c]..seg_ptr[c+1]) in output order
+ * and the representatives rep_region[rep_ptr[c]..rep_ptr[c+1]) (one per chromosome,
+ * drawn by the caller as sprite.pyx:231 does); seg_rep[g] is the slot of segment
+ * g's chromosome among its cluster's representatives.  A cluster without
+ * representatives is a single-chromosome cluster (every copy k is one group).
+ * Outputs: rg2_out (ncluster, nstruct) f32 (nullable); best_idx/best_rg2
+ * (ncluster, keep_best); best_sel: cluster c's (keep_best, nseg_c) selected beads at
+ * offset seg_ptr[c] * keep_best.  Host pointers only (the CSR arrays are validated). */
+int igm_sprite_assign(igm_ctx* ctx, uint32_t flags,
+                      const float* xyz, int32_t nbead, int32_t nstruct,
+                      int32_t ncluster, const int32_t* seg_ptr, const int32_t* seg_region,
+                      const int32_t* seg_rep, const int32_t* rep_ptr, const int32_t* rep_region,
+                      int32_t nregion, const int32_t* alt_ptr, const int32_t* alt_bead,
+                      int32_t keep_best, float* rg2_out,
+                      int32_t* best_idx, float* best_rg2, int32_t* best_sel);
+
 /* ---- M-step ---------------------------------------------------------------
  * Batched replacement of lammps.optimize (lammps.py:361-492): the protocol of
  * create_lammps_script (lammps.py:149-358) -- per stage: fix adapt of the soft
