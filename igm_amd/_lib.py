@@ -24,6 +24,7 @@ IGM_DEVICE_PTRS = 0x1
 IGM_ASYNC = 0x2
 IGM_F32_PATH = 0x4
 IGM_MSTEP_FORCE_GLOBAL = 0x1  # igm_mstep_params.flags: HBM-resident kernels even when LDS fits
+IGM_MSTEP_STRUCT_FLAGS = 0x2  # igm_mstep_params.flags: atom_flags is (nstruct, natom)
 
 IGM_MAX_STAGES = 16
 IGM_MAX_ENVELOPES = 4
@@ -99,6 +100,7 @@ SIGNATURES = {
     'igm_astep_update_plast': (_i32, [_vp, _u32, _vp, _i64, _vp]),
     'igm_damid_actdist': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _f64,
                                  _i32, _vp, _vp, _vp, _i64, ctypes.POINTER(_i64)]),
+    'igm_damid_select': (_i32, [_vp, _u32, _i32, _i32, _vp, _vp, _vp, _i64, _vp, _f64, _u32, _vp, _vp, _vp]),
     'igm_fish_assign': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp,
                                _vp, _vp]),
     'igm_sprite_assign': (_i32, [_vp, _u32, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32,

@@ -30,6 +30,7 @@ SOURCES = {
     'hic_select.hip': ['-ffp-contract=off'],
     'violations.hip': ['-ffp-contract=off'],
     'asteps.hip': ['-ffp-contract=off'],
+    'restraints.hip': ['-ffp-contract=off'],
 }
 COMMON = ['-O3', '-fPIC', '-std=c++17', '--offload-arch=%s' % ARCH, '-Wall', '-Wno-unused-function',
           '-munsafe-fp-atomics', '-I%s' % os.path.join(ROOT, 'include')]

@@ -89,7 +89,8 @@ struct Common {
     int nstruct, natom, nslice, ldn;  // ldn: SoA stride of per-atom HBM arrays (natom rounded to 64)
     const float* radii;
     const int* atype;  // per atom: index into DevParams::pair_tab / rtype
-    const uint32_t* aflags;
+    const uint32_t* aflags;  // (natom), or (nstruct, natom) when afs == natom
+    size_t afs;              // aflags stride between structures (0: shared by all)
     Bonds bonds;
     int* work_counter;  // dynamic structure scheduler
     int* error;         // error bits (per launch)
@@ -668,7 +669,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
         for (int b = 0; b < BPT; ++b) {
             const int a = b * NT + t;
             const bool in = a < natom;
-            const uint32_t fl = in ? A.cm.aflags[a] : 0u;
+            const uint32_t fl = in ? A.cm.aflags[(size_t)s * A.cm.afs + a] : 0u;
             const bool bead = in && (fl & IGM_ATOM_BEAD);
             if (in && !(fl & IGM_ATOM_FIXED)) {
                 mobile |= 1u << b;
@@ -774,7 +775,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                         const BondView B = lds_bonds ? BondView{nullptr, nullptr, sm.rest + sm.boff[a], sm.btab,
                                                                 (int)sm.boff[a + 1] - (int)sm.boff[a]}
                                                      : BondView{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
-                        atom_force<float, false, uint16_t>(a, sm.pos[a], A.cm.aflags[a], sm.pos, sm.L,
+                        atom_force<float, false, uint16_t>(a, sm.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], sm.pos, sm.L,
                                                            pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
                                                            pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz, ep,
                                                            eb, ee);
@@ -870,6 +871,7 @@ struct PopArgs {
     double* kep;        // (B, nbs) per-block kinetic-energy partials (2x KE, mass 1)
     float* bbp;         // (B, nbs, 6) per-block bounding-box partials {max -x, -y, -z, max x, y, z}
     int* ncell;         // (B) cells of the structure's current grid
+    const double* dofs; // (B) dof of group nonfixed
     int nbs;
 };
 
@@ -901,7 +903,7 @@ __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float
     if (a >= A.cm.natom) return;
     const size_t i = (size_t)s * A.cm.ldn + a;
     const float* x = xyz + ((size_t)s * A.cm.natom + a) * 3;
-    const uint32_t fl = A.cm.aflags[a];
+    const uint32_t fl = A.cm.aflags[(size_t)s * A.cm.afs + a];
     const float r = A.cm.radii[a];
     W.pos[a] = make_float4(x[0], x[1], x[2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
     A.v4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -916,7 +918,7 @@ __global__ void __launch_bounds__(kPopBS) pop_setvel_kernel(PopArgs A, const flo
     if (s >= A.cm.nstruct) return;
     if (a >= A.cm.natom) return;
     const float* v = vsrc + (size_t)s * sstride + (size_t)a * 3;
-    const bool mob = !(A.cm.aflags[a] & IGM_ATOM_FIXED);
+    const bool mob = !(A.cm.aflags[(size_t)s * A.cm.afs + a] & IGM_ATOM_FIXED);
     A.v4[(size_t)s * A.cm.ldn + a] = mob ? make_float4(v[0], v[1], v[2], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
@@ -926,7 +928,6 @@ struct PopStep {
     int rescale;      // apply the temp/rescale of step `prev` first
     int prev, nsteps;
     float t0, t1, window, fraction;
-    double dof;
 };
 
 // temp/rescale factor of structure s at the end of step P.prev (fixed-order sum of partials)
@@ -935,7 +936,7 @@ __device__ __forceinline__ float pop_factor(const PopArgs& A, const PopStep& S, 
         double ke = 0.0;
         const double* kp = A.kep + (size_t)s * A.nbs;
         for (int i = 0; i < A.nbs; ++i) ke += kp[i];
-        *shared = temp_rescale_factor(ke, S.dof, S.prev, S.nsteps, S.t0, S.t1, S.window, S.fraction);
+        *shared = temp_rescale_factor(ke, A.dofs[s], S.prev, S.nsteps, S.t0, S.t1, S.window, S.fraction);
     }
     __syncthreads();
     return *shared;
@@ -955,7 +956,7 @@ __global__ void __launch_bounds__(kPopBS) pop_kick_drift_kernel(PopArgs A, PopSt
     if (a < A.cm.natom) {
         const size_t i = (size_t)s * A.cm.ldn + a;
         float4 p = W.pos[a];
-        if (S.integrate && !(A.cm.aflags[a] & IGM_ATOM_FIXED)) {
+        if (S.integrate && !(A.cm.aflags[(size_t)s * A.cm.afs + a] & IGM_ATOM_FIXED)) {
             float4 v = A.v4[i];
             const float4 f = A.f4[i];
             v.x *= factor;
@@ -1141,7 +1142,7 @@ __global__ void __launch_bounds__(kPopBS) pop_forces_kernel(PopArgs A, float evf
     const float4 b = A.xb4[i];
     double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
     float fx, fy, fz;
-    atom_force<float, false, int>(a, W.pos[a], A.cm.aflags[a], W.pos, L, b.x, b.y, b.z, B, A.P, evf, envf, fx, fy,
+    atom_force<float, false, int>(a, W.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], W.pos, L, b.x, b.y, b.z, B, A.P, evf, envf, fx, fy,
                                   fz, ep, eb, ee);
     A.f4[i] = make_float4(fx, fy, fz, 0.f);
 }
@@ -1152,7 +1153,7 @@ __global__ void __launch_bounds__(kPopBS) pop_kick_kernel(PopArgs A, PopStep S) 
     const int lb = pop_block(A), s = lb / A.nbs, blk = lb % A.nbs, a = blk * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
     double ke = 0.0;
-    if (a < A.cm.natom && !(A.cm.aflags[a] & IGM_ATOM_FIXED)) {
+    if (a < A.cm.natom && !(A.cm.aflags[(size_t)s * A.cm.afs + a] & IGM_ATOM_FIXED)) {
         const size_t i = (size_t)s * A.cm.ldn + a;
         float4 v = A.v4[i];
         const float4 f = A.f4[i];
@@ -1213,6 +1214,7 @@ __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S
 struct VelArgs {
     int nstruct, natom, nseg;
     const uint32_t* aflags;
+    size_t afs;                    // aflags stride between structures (0: shared)
     const int* seeds;              // (B) stage-0 seed
     int seg_stage[2 * IGM_MAX_STAGES];
     float seg_temp[2 * IGM_MAX_STAGES];
@@ -1224,9 +1226,10 @@ __global__ void __launch_bounds__(256) velocity_kernel(VelArgs V) {
     const int seg = blockIdx.x, s = blockIdx.y, t = threadIdx.x;
     const uint32_t seed = (uint32_t)(V.seeds[s] + V.seg_stage[seg]);
     float* out = V.vinit + ((size_t)s * V.nseg + seg) * V.natom * 3;
+    const uint32_t* vfl = V.aflags + (size_t)s * V.afs;
     double s4[4] = {0, 0, 0, 0};
     for (int a = t; a < V.natom; a += 256) {
-        if (V.aflags[a] & IGM_ATOM_FIXED) continue;
+        if (vfl[a] & IGM_ATOM_FIXED) continue;
 #pragma unroll
         for (int d = 0; d < 3; ++d) s4[d] += ranpark_nth(seed, 3ull * a + d + 1) - 0.5;
         s4[3] += 1.0;
@@ -1236,7 +1239,7 @@ __global__ void __launch_bounds__(256) velocity_kernel(VelArgs V) {
     const double nmob = s4[3];
     double t2[1] = {0.0};
     for (int a = t; a < V.natom; a += 256) {
-        if (V.aflags[a] & IGM_ATOM_FIXED) continue;
+        if (vfl[a] & IGM_ATOM_FIXED) continue;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             const double vd = (ranpark_nth(seed, 3ull * a + d + 1) - 0.5) - s4[d] / nmob;
@@ -1248,7 +1251,7 @@ __global__ void __launch_bounds__(256) velocity_kernel(VelArgs V) {
     const double tc = dof > 0 ? t2[0] / dof : 0.0;
     const double factor = tc > 0.0 ? sqrt((double)V.seg_temp[seg] / tc) : 0.0;
     for (int a = t; a < V.natom; a += 256) {
-        const bool fixed = V.aflags[a] & IGM_ATOM_FIXED;
+        const bool fixed = vfl[a] & IGM_ATOM_FIXED;
 #pragma unroll
         for (int d = 0; d < 3; ++d)
             out[(size_t)a * 3 + d] =
@@ -1336,7 +1339,7 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
         if (s >= A.cm.nstruct) break;
         const float* xs = A.xyz + (size_t)s * natom * 3;
         for (int a = t; a < natom; a += NT) {
-            const uint32_t fl = A.cm.aflags[a];
+            const uint32_t fl = A.cm.aflags[(size_t)s * A.cm.afs + a];
             const double r = (double)A.cm.atype[a];
             pos[a] = make_double4((double)xs[(size_t)a * 3], (double)xs[(size_t)a * 3 + 1],
                                   (double)xs[(size_t)a * 3 + 2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0));
@@ -1390,7 +1393,7 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
                 double e_e[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
                 double fx, fy, fz;
                 const BondView B{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
-                atom_force<double, true, int>(a, pos[a], A.cm.aflags[a], pos, L, XB[a], XB[ldn + a],
+                atom_force<double, true, int>(a, pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], pos, L, XB[a], XB[ldn + a],
                                               XB[2 * ldn + a], B, A.P, A.evf, A.envf, fx, fy, fz, vv[0], vv[1], e_e);
                 for (int e = 0; e < IGM_MAX_ENVELOPES; ++e) vv[2 + e] += e_e[e];
                 F[a] = fx;
@@ -1919,7 +1922,20 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
     const int64_t* d_sptr;
     const igm_bond* d_sb;
     IGM_TRY(to_device(c, flags, "ms_radii", radii, (size_t)natom, &d_radii));
-    IGM_TRY(to_device(c, flags, "ms_flags", atom_flags, (size_t)natom, &d_flags));
+    // IGM_MSTEP_STRUCT_FLAGS: one flag row per structure (DamID envelope membership,
+    // SPRITE centroid slots); the BEAD bit must agree between structures
+    const bool per_struct = (prm->flags & IGM_MSTEP_STRUCT_FLAGS) != 0;
+    const size_t nfl = per_struct ? (size_t)nstruct * natom : (size_t)natom;
+    IGM_TRY(to_device(c, flags, "ms_flags", atom_flags, nfl, &d_flags));
+    if (per_struct) {
+        std::vector<uint32_t> fl(nfl);
+        IGM_HIP_CHECK(c, hipMemcpyAsync(fl.data(), d_flags, sizeof(uint32_t) * nfl, hipMemcpyDeviceToHost, c->stream));
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+        for (size_t k = natom; k < nfl; ++k)
+            if ((fl[k] ^ fl[k % natom]) & IGM_ATOM_BEAD)
+                return fail(c, IGM_E_INVALID, "per-structure atom flags: atom %d is a bead in one structure only",
+                            (int)(k % natom));
+    }
     IGM_TRY(to_device(c, flags, "ms_shared", shared_bonds, (size_t)nshared, &d_shared));
     int64_t nsb = 0;
     if (sbond_ptr) {
@@ -2010,6 +2026,7 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
     out->cm.radii = d_radii;
     out->cm.atype = d_atype;
     out->cm.aflags = d_flags;
+    out->cm.afs = per_struct ? (size_t)natom : 0;
     out->cm.bonds.base = (const int64_t*)p_base;
     out->cm.bonds.soff = (const int*)p_soff;
     out->cm.bonds.deg = (const int*)p_deg;
@@ -2093,12 +2110,26 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.bbp = (float*)pbb;
     Q.ncell = (int*)pnc;
     Q.nrebuild = (int*)pnr;
-    // dof of group nonfixed (flags are shared by the structures)
-    std::vector<uint32_t> fl(N);
-    IGM_HIP_CHECK(c, hipMemcpyAsync(fl.data(), pr.cm.aflags, sizeof(uint32_t) * N, hipMemcpyDeviceToHost, c->stream));
-    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
-    int nmob = 0;
-    for (int i = 0; i < N; ++i) nmob += (fl[i] & IGM_ATOM_FIXED) ? 0 : 1;
+    // dof of group nonfixed, per structure (atom flags may differ between structures)
+    {
+        const size_t nfl = pr.cm.afs ? (size_t)S * N : (size_t)N;
+        std::vector<uint32_t> fl(nfl);
+        IGM_HIP_CHECK(c, hipMemcpyAsync(fl.data(), pr.cm.aflags, sizeof(uint32_t) * nfl, hipMemcpyDeviceToHost,
+                                        c->stream));
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+        std::vector<double> dofs(S);
+        for (int st = 0; st < S; ++st) {
+            const uint32_t* f = fl.data() + (size_t)st * pr.cm.afs;
+            int nmob = 0;
+            for (int i = 0; i < N; ++i) nmob += (f[i] & IGM_ATOM_FIXED) ? 0 : 1;
+            dofs[st] = 3.0 * nmob - 3.0;
+        }
+        void* pdof;
+        IGM_TRY(workspace(c, "pop_dof", sizeof(double) * S, &pdof));
+        IGM_HIP_CHECK(c, hipMemcpyAsync(pdof, dofs.data(), sizeof(double) * S, hipMemcpyHostToDevice, c->stream));
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+        Q.dofs = (const double*)pdof;
+    }
     const dim3 grid((S * Q.nbs + 7) & ~7), blk(kPopBS);  // padded for pop_block
     Timed tm(c, "anneal");
     hipLaunchKernelGGL(pop_load_kernel, grid, blk, 0, c->stream, Q, (const float*)A.xyz);
@@ -2123,7 +2154,6 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         st.t1 = A.seg_t1[seg];
         st.window = A.t_window;
         st.fraction = A.t_fraction;
-        st.dof = 3.0 * nmob - 3.0;
         const float evf = A.seg_evf[seg], envf = A.seg_envf[seg];
         for (int step = 0; step <= st.nsteps; ++step) {
             st.integrate = step > 0;
@@ -2211,6 +2241,7 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
             V.natom = pr.cm.natom;
             V.nseg = n;
             V.aflags = pr.cm.aflags;
+            V.afs = pr.cm.afs;
             V.seeds = d_seeds;
             V.vinit = (float*)pv;
             Timed tm(c, "velocity");

@@ -42,6 +42,7 @@ struct VArgs {
     const float* xyz;
     const float* radii;
     const uint32_t* aflags;
+    size_t afs;  // aflags stride between structures (IGM_MSTEP_STRUCT_FLAGS) or 0
     const igm_bond* shared;
     const int32_t* shared_class;
     int64_t nshared;
@@ -89,7 +90,7 @@ __global__ void __launch_bounds__(256) violations_kernel(VArgs A) {
     for (int e = 0; e < A.nenv; ++e) {
         int* he = &h[(A.nclass_bonds + e) * kRec];
         for (int a = t; a < A.natom; a += 256) {
-            if (!(A.aflags[a] & (IGM_ATOM_ENV0 << e))) continue;
+            if (!(A.aflags[(size_t)s * A.afs + a] & (IGM_ATOM_ENV0 << e))) continue;
             const float* p = x + 3 * a;
             const double r = (double)A.radii[a];
             double acc = 0.0;
@@ -154,7 +155,8 @@ extern "C" int igm_mstep_violations(igm_ctx* c, uint32_t flags, const igm_mstep_
     }
     IGM_TRY(to_device(c, flags, "vi_xyz", xyz, (size_t)nstruct * natom * 3, &A.xyz));
     IGM_TRY(to_device(c, flags, "vi_radii", radii, (size_t)natom, &A.radii));
-    IGM_TRY(to_device(c, flags, "vi_flags", atom_flags, (size_t)natom, &A.aflags));
+    A.afs = (prm->flags & IGM_MSTEP_STRUCT_FLAGS) ? (size_t)natom : 0;
+    IGM_TRY(to_device(c, flags, "vi_flags", atom_flags, A.afs ? (size_t)nstruct * natom : (size_t)natom, &A.aflags));
     IGM_TRY(to_device(c, flags, "vi_shared", shared_bonds, (size_t)nshared, &A.shared));
     IGM_TRY(to_device(c, flags, "vi_shcls", shared_class, shared_class ? (size_t)nshared : 0, &A.shared_class));
     IGM_TRY(to_device(c, flags, "vi_sptr", sbond_ptr, sbond_ptr ? (size_t)nstruct + 1 : 0, &A.sptr));

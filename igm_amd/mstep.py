@@ -31,6 +31,16 @@ def _np(a, dt):
     return np.ascontiguousarray(a, dtype=dt)
 
 
+def _prm(params, flags):
+    """params with IGM_MSTEP_STRUCT_FLAGS set when flags has one row per structure."""
+    nd = flags.dim() if hasattr(flags, 'dim') else np.ndim(flags)
+    if nd != 2:
+        return params
+    p = _lib.MStepParams.from_buffer_copy(params)
+    p.flags |= _lib.IGM_MSTEP_STRUCT_FLAGS
+    return p
+
+
 def _bonds_args(shared, sptr, sbonds, nstruct):
     shared = _np(shared if shared is not None else np.zeros(0, bond_dtype), bond_dtype)
     if sbonds is None or sptr is None:
@@ -48,8 +58,9 @@ def run(params, xyz, radii, flags, shared_bonds, sbond_ptr, sbonds, seeds, ctx=N
         S, N = int(xyz.shape[0]), int(xyz.shape[1])
         info = torch.empty(S * optinfo_dtype.itemsize, dtype=torch.uint8, device=xyz.device)
         c.set_stream(torch.cuda.current_stream(xyz.device).cuda_stream)
+        prm = _prm(params, flags)
         try:
-            rc = c.lib.igm_mstep_run(c.h, IGM_DEVICE_PTRS, ctypes.byref(params), S, N, _lib.ptr(xyz),
+            rc = c.lib.igm_mstep_run(c.h, IGM_DEVICE_PTRS, ctypes.byref(prm), S, N, _lib.ptr(xyz),
                                      _lib.ptr(radii), _lib.ptr(flags), _lib.ptr(shared_bonds),
                                      int(shared_bonds.shape[0]) // bond_dtype.itemsize
                                      if shared_bonds.dtype == torch.uint8 else int(shared_bonds.shape[0]),
@@ -64,9 +75,11 @@ def run(params, xyz, radii, flags, shared_bonds, sbond_ptr, sbonds, seeds, ctx=N
     flags = _np(flags, np.uint32)
     seeds = _np(seeds, np.int32)
     shared, sptr, sb = _bonds_args(shared_bonds, sbond_ptr, sbonds, S)
-    assert radii.shape[0] == N and flags.shape[0] == N and seeds.shape[0] == S
+    assert radii.shape[0] == N and flags.shape[-1] == N and seeds.shape[0] == S
+    assert flags.ndim == 1 or flags.shape[0] == S, 'per-structure flags must be (S, N)'
+    prm = _prm(params, flags)
     info = np.zeros(S, optinfo_dtype)
-    rc = c.lib.igm_mstep_run(c.h, 0, ctypes.byref(params), S, N, xyz.ctypes.data, radii.ctypes.data,
+    rc = c.lib.igm_mstep_run(c.h, 0, ctypes.byref(prm), S, N, xyz.ctypes.data, radii.ctypes.data,
                              flags.ctypes.data, shared.ctypes.data if len(shared) else None, len(shared),
                              _lib.ptr(sptr), _lib.ptr(sb), seeds.ctypes.data, info.ctypes.data)
     c.check(rc, 'igm_mstep_run')
@@ -81,7 +94,8 @@ def forces(params, xyz, radii, flags, shared_bonds, sbond_ptr, sbonds, evf, envf
     shared, sptr, sb = _bonds_args(shared_bonds, sbond_ptr, sbonds, S)
     f = np.zeros((S, N, 3), np.float32)
     e = np.zeros((S, 7), np.float64)
-    rc = c.lib.igm_mstep_forces(c.h, IGM_F32_PATH if f32 else 0, ctypes.byref(params), S, N, xyz.ctypes.data,
+    prm = _prm(params, flags)
+    rc = c.lib.igm_mstep_forces(c.h, IGM_F32_PATH if f32 else 0, ctypes.byref(prm), S, N, xyz.ctypes.data,
                                 _np(radii, np.float32).ctypes.data, _np(flags, np.uint32).ctypes.data,
                                 shared.ctypes.data if len(shared) else None, len(shared), _lib.ptr(sptr),
                                 _lib.ptr(sb), float(evf), float(envf), f.ctypes.data, e.ctypes.data)
@@ -97,7 +111,8 @@ def md(params, xyz, v, radii, flags, shared_bonds, sbond_ptr, sbonds, evf, envf,
     v = np.array(v, np.float32, order='C', copy=True)
     S, N = xyz.shape[0], xyz.shape[1]
     shared, sptr, sb = _bonds_args(shared_bonds, sbond_ptr, sbonds, S)
-    rc = c.lib.igm_mstep_md(c.h, 0, ctypes.byref(params), S, N, xyz.ctypes.data, v.ctypes.data,
+    prm = _prm(params, flags)
+    rc = c.lib.igm_mstep_md(c.h, 0, ctypes.byref(prm), S, N, xyz.ctypes.data, v.ctypes.data,
                             _np(radii, np.float32).ctypes.data, _np(flags, np.uint32).ctypes.data,
                             shared.ctypes.data if len(shared) else None, len(shared), _lib.ptr(sptr),
                             _lib.ptr(sb), float(evf), float(envf), float(t0), float(t1), float(xmax), int(nsteps))
@@ -165,7 +180,8 @@ def violations(params, xyz, radii, flags, shared_bonds, shared_class, sbond_ptr,
     esc = _np(env_scale, np.float64) if env_scale is not None else None
     ncls = len(ccr) + params.nenvelopes
     stats = np.zeros((S, ncls, REC), np.int64)
-    rc = c.lib.igm_mstep_violations(c.h, 0, ctypes.byref(params), S, N, xyz.ctypes.data,
+    prm = _prm(params, flags)
+    rc = c.lib.igm_mstep_violations(c.h, 0, ctypes.byref(prm), S, N, xyz.ctypes.data,
                                     _np(radii, np.float32).ctypes.data, _np(flags, np.uint32).ctypes.data,
                                     shared.ctypes.data if len(shared) else None, _lib.ptr(shc), len(shared),
                                     _lib.ptr(sptr), _lib.ptr(sb), _lib.ptr(scl), len(ccr), ccr.ctypes.data,

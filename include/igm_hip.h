@@ -161,6 +161,19 @@ int igm_sprite_assign(igm_ctx* ctx, uint32_t flags,
                       int32_t keep_best, float* rg2_out,
                       int32_t* best_idx, float* best_rg2, int32_t* best_sel);
 
+/* DamID lamina envelope membership (M-step restraint assembly, config D):
+ * Damid._apply_envelope (igm/restraints/damid.py:112-143) for every structure at once.
+ * out_flags[s, a] = base_flags[a] | (env_bit if some DamID row {loc = a, dist = d}
+ * has snormsq_ellipsoid(x_sa, semiaxes * (1 - contact_range), r_a) >= d^2), bit-exact
+ * with the reference's NumPy 1.x arithmetic.  xyz is the M-step layout
+ * (nstruct, natom, 3); the result feeds igm_mstep_run with IGM_MSTEP_STRUCT_FLAGS and
+ * an envelope whose k is -contact_kspring.  n_selected (nullable): rows selected per
+ * structure (the restraint's rnum). */
+int igm_damid_select(igm_ctx* ctx, uint32_t flags, int32_t nstruct, int32_t natom, const float* xyz,
+                     const float* radii, const igm_damid_row* rows, int64_t nrows,
+                     const double* semiaxes, double contact_range, uint32_t env_bit,
+                     const uint32_t* base_flags, uint32_t* out_flags, int32_t* n_selected);
+
 /* ---- M-step ---------------------------------------------------------------
  * Batched replacement of lammps.optimize (lammps.py:361-492): the protocol of
  * create_lammps_script (lammps.py:149-358) -- per stage: fix adapt of the soft
@@ -201,6 +214,9 @@ typedef struct {
 
 /* igm_mstep_params.flags */
 #define IGM_MSTEP_FORCE_GLOBAL 0x1 /* use the HBM-resident kernels even when a structure fits in LDS */
+#define IGM_MSTEP_STRUCT_FLAGS 0x2 /* atom_flags is (nstruct, natom): per-structure envelope membership
+                                      (DamID) and active/inactive centroid slots (SPRITE); the
+                                      IGM_ATOM_BEAD bit must be the same in every structure */
 
 /* atom flags (per atom, shared by all structures of a batch) */
 #define IGM_ATOM_BEAD 0x1u   /* takes part in the soft pair potential       */
@@ -225,7 +241,7 @@ typedef struct {
 
 /* Run the whole protocol for `nstruct` structures of `natom` atoms each.
  *   xyz       (nstruct, natom, 3) f32, in/out
- *   radii     (natom) f32; atom_flags (natom)
+ *   radii     (natom) f32; atom_flags (natom), or (nstruct, natom) with IGM_MSTEP_STRUCT_FLAGS
  *   bonds     shared bonds (polymer) + per-structure bonds (Hi-C ...):
  *             shared_bonds[nshared]; sbond_ptr[nstruct+1] into sbonds[]
  *   seeds     (nstruct) LAMMPS 'velocity create' seed of stage 0 (stage k: +k)
