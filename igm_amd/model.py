@@ -154,3 +154,84 @@ def concat_bonds(per_struct):
     ptr[1:] = np.cumsum([len(b) for b in per_struct])
     bonds = np.concatenate(per_struct) if len(per_struct) else np.zeros(0, bond_dtype)
     return ptr, np.ascontiguousarray(bonds, bond_dtype)
+
+
+# ---- LammpsModel.from_model for a reference igm Model object --------------------
+class LammpsLikeModel(object):
+    """The arrays LammpsModel.from_model (igm/model/kernel/lammps_model.py:244-301)
+    derives from an igm Model: atoms (radii, flags, xyz), bonds, envelopes, evfactor,
+    and imap (particle index -> atom index)."""
+
+    def __init__(self, radii, flags, xyz, bonds, envelopes, evfactor, imap, uid):
+        self.radii, self.flags, self.xyz, self.bonds = radii, flags, xyz, bonds
+        self.envelopes, self.evfactor, self.imap, self.id = envelopes, evfactor, imap, uid
+
+
+# Force.ftype codes (igm/model/forces.py:14-18) and Particle.ptype codes (particle.py:11-13)
+_EXCLUDED_VOLUME, _UPPER, _LOWER, _ENVELOPE, _GENERAL_ENVELOPE = 0, 1, 2, 3, 4
+_NORMAL, _DUMMY_STATIC, _DUMMY_DYNAMIC = 0, 1, 2
+_DUMMY_MAX_BONDS = 20  # FrozenPhantomBead.MAX_BONDS (lammps_model.py:177)
+
+
+def from_igm_model(model):
+    """LammpsModel.from_model semantics on a reference `igm.model.Model` (duck typed:
+    .id, .particles[.pos, .r, .ptype], .forces[.ftype, .i, .j, .d, .k | .particle_ids,
+    .semiaxes, .shape]):
+      NORMAL -> bead atom; DUMMY_STATIC -> frozen dummy, merged into the previous atom
+      when that is a dummy at the same position (get_next_dummy, :303-312);
+      DUMMY_DYNAMIC -> mobile centroid without pair interactions;
+      HARMONIC_UPPER/LOWER_BOUND -> bonds in force order; EXCLUDED_VOLUME -> evfactor;
+      ENVELOPE -> envelope (only those with particles get a LAMMPS group, lammps.py:231-233).
+    Volumetric (exp_map) envelopes are out of scope and raise NotImplementedError."""
+    radii, flags, xyz, imap = [], [], [], []
+    for p in model.particles:
+        pos = np.asarray(p.pos, np.float32)
+        if p.ptype == _NORMAL:
+            radii.append(np.float32(p.r))
+            flags.append(IGM_ATOM_BEAD)
+            xyz.append(pos)
+        elif p.ptype == _DUMMY_STATIC:
+            if flags and flags[-1] == IGM_ATOM_FIXED and np.all(xyz[-1] == pos):
+                imap.append(len(flags) - 1)
+                continue
+            radii.append(np.float32(0.0))
+            flags.append(IGM_ATOM_FIXED)
+            xyz.append(pos)
+        elif p.ptype == _DUMMY_DYNAMIC:
+            radii.append(np.float32(0.0))
+            flags.append(0)
+            xyz.append(pos)
+        else:
+            raise ValueError('Unknown particle type')
+        imap.append(len(flags) - 1)
+    flags = np.asarray(flags, np.uint32)
+    imap = np.asarray(imap, np.int64)
+    bi, bj, br, bk, lower, envelopes, evfactor = [], [], [], [], [], [], 1.0
+    for f in model.forces:
+        if f.ftype in (_ENVELOPE, _GENERAL_ENVELOPE):
+            if getattr(f, 'shape', 'ellipsoid') != 'ellipsoid':
+                raise NotImplementedError('envelope shape %s (volumetric maps are out of scope)' % f.shape)
+            if len(f.particle_ids):
+                e = len(envelopes)
+                if e >= IGM_MAX_ENVELOPES:
+                    raise ValueError('at most %d envelopes' % IGM_MAX_ENVELOPES)
+                flags[imap[np.asarray(f.particle_ids, np.int64)]] |= np.uint32(IGM_ATOM_ENV0 << e)
+                envelopes.append((tuple(float(v) for v in f.semiaxes), float(f.k)))
+        elif f.ftype == _EXCLUDED_VOLUME:
+            evfactor = float(f.k)
+        elif f.ftype in (_UPPER, _LOWER):
+            bi.append(imap[f.i])
+            bj.append(imap[f.j])
+            br.append(f.d)
+            bk.append(f.k)
+            lower.append(f.ftype == _LOWER)
+        else:
+            raise ValueError('Unknown force type %r' % f.ftype)
+    bonds = np.zeros(len(bi), bond_dtype)
+    if len(bi):
+        bonds['i'] = bi
+        bonds['j'] = np.asarray(bj, np.uint32) | np.where(lower, LOWER_BOUND_BIT, np.uint32(0)).astype(np.uint32)
+        bonds['r0'] = br
+        bonds['k'] = bk
+    return LammpsLikeModel(np.asarray(radii, np.float32), flags, np.stack(xyz).astype(np.float32), bonds,
+                           envelopes, evfactor, imap, getattr(model, 'id', 0))
