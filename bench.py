@@ -41,6 +41,8 @@ def parse():
     ap.add_argument('--sigma', type=float, default=None, help='Hi-C sigma (B: 0.02, C: 0.01)')
     ap.add_argument('--cpu-sample', type=int, default=16, help='structures in the CPU baseline sample (0: skip)')
     ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--no-de', action='store_true', help='skip the configuration D/E A-step measurement')
+    ap.add_argument('--sprite-clusters', type=int, default=20000, help='SPRITE clusters in the D/E measurement')
     ap.add_argument('--protocol-scale', type=float, default=1.0,
                     help='scale the MD step counts (only for smoke tests; the metric needs 1.0)')
     a = ap.parse_args()
@@ -100,6 +102,70 @@ def cpu_baseline(args, it, inp):
                       % (n, dt)}
 
 
+def bench_asteps_de(args, ctx):
+    """Configuration D/E A-steps at full population size (200 kb diploid, 1000
+    structures, bead-major .hss layout resident in HBM), timed with HIP events around
+    each kernel family: DamID (ellipsoid, sigma 0.45), FISH (500 probes + 500 pairs),
+    SPRITE (Rg^2 of every (cluster, structure) + keep_best 50).  Outside the timed
+    A/M region; reported beside it.  Algorithmic bytes: the unique coordinate columns
+    each unit reads (12 B per bead per structure) plus its inputs/outputs."""
+    import torch
+    from igm_amd import damid, fish, sprite, synthetic as syn
+    S = 1000
+    pop = syn.population_200kb(S)
+    xyz = np.ascontiguousarray(pop['xyz'].transpose(1, 0, 2))
+    cp, ci = pop['copy_ptr'], pop['copy_idx']
+    nc = np.diff(cp)
+    out = {}
+    loci, pe, pl = damid.select_loci(syn.damid_profile_200kb(), 0.45)
+    pl[::2] = np.float32(0.3)
+    for _ in range(2):  # first call stages the population; time the second
+        damid.compute_damid_actdist(xyz, pop['radii'], cp, ci, loci, pe, pl, 1, 0.05, 'ellipsoid',
+                                    syn.ELLIPSOID_D, ctx=ctx)
+    ms = ctx.kernel_ms('damid')
+    b = float((12.0 * S * nc[loci] + 12.0 * nc[loci] + 8).sum())
+    out['damid'] = {'units': int(len(loci)), 'unit': 'loci', 'ms': ms, 'algorithmic_bytes': b,
+                    'achieved_GBps': b / (ms * 1e-3) / 1e9}
+    f = syn.fish_inputs_200kb(S)
+    tot_ms, tot_b = 0.0, 0.0
+    for kind, key, pre in (('probe', 'probes', 'radial'), ('pair', 'pairs', 'pair')):
+        for _ in range(2):
+            fish.assign(xyz, cp, ci, kind, f[key], f[pre + '_min'], f[pre + '_max'], ctx=ctx)
+        tot_ms += ctx.kernel_ms('fish')
+        cols = nc[f[key]] if kind == 'probe' else nc[f[key][:, 0]] + nc[f[key][:, 1]]
+        tot_b += float((12.0 * S * cols + 16.0 * S).sum())
+    out['fish'] = {'units': int(len(f['probes']) + len(f['pairs'])), 'unit': 'probes+pairs', 'ms': tot_ms,
+                   'algorithmic_bytes': tot_b, 'achieved_GBps': tot_b / (tot_ms * 1e-3) / 1e9}
+    ptr, data = syn.sprite_clusters_200kb(args.sprite_clusters)
+    cl = [data[ptr[c]:ptr[c + 1]] for c in range(len(ptr) - 1)]
+    t = sprite.cluster_tables(cl, pop['hap_chrom'], cp, rng=np.random.RandomState(0))
+    for _ in range(2):
+        sprite.rg2_select(xyz, cp, ci, t, 50, ctx=ctx)
+    ms = ctx.kernel_ms('sprite')
+    alts = nc[t['seg_region']].sum() + (nc[t['rep_region']].sum() if len(t['rep_region']) else 0)
+    b = float(12.0 * S * alts + 4.0 * S * len(t['kept']) * 2 + 4.0 * S * len(t['seg_region']) +
+              (4 + 4) * 50 * len(t['kept']) + 4 * 50 * len(t['seg_region']))
+    out['sprite'] = {'units': int(len(t['kept'])), 'unit': 'clusters x 1000 structures', 'ms': ms,
+                     'algorithmic_bytes': b, 'achieved_GBps': b / (ms * 1e-3) / 1e9}
+    out['workload'] = '200 kb diploid (29 838 beads), 1000 structures, bead-major f32 in HBM'
+    del torch
+    return out
+
+
+def measured_traffic(config):
+    """HBM bytes per anneal launch from the committed PMC passes (FETCH_SIZE x 2 gfx950
+    correction + WRITE_SIZE, scripts/gpu_bench.sh -> profiles/<round>/hbm_traffic.txt),
+    kept in bench_traffic.json beside this file; None when not measured."""
+    path = os.path.join(ROOT, 'bench_traffic.json')
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as fh:
+        d = json.load(fh).get(config)
+    if not d:
+        return None, None
+    return float(d['fetch_bytes_per_launch']) + float(d['write_bytes_per_launch']), d['source']
+
+
 def main():
     args = parse()
     import torch
@@ -149,6 +215,9 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    de = None
+    if rank == 0 and not args.no_de:
+        de = bench_asteps_de(args, it.ctx)
     score = it.violation_score()
     info = it.info_host()
     ms_per_step = 1000.0 * dt / max(args.steps, 1)
@@ -156,6 +225,7 @@ def main():
     value = total * args.steps / dt
     a_ms = float(np.mean(anneal_ms)) if anneal_ms else float('nan')
     achieved = float(np.mean(bytes_launch)) / (a_ms * 1e-3) / 1e9 if anneal_ms else 0.0
+    traffic, traffic_src = measured_traffic(args.config)
     if rank == 0:
         line = {
             'metric': 'M-step structures/sec + A/M iteration wall-time (BASELINE.json), %s' % (
@@ -173,10 +243,12 @@ def main():
                        'nstruct_per_gpu': it.S_local, 'nstruct_total': total, 'sigma': args.sigma,
                        'npairs': int(it.npairs_total), 'parallelism': 'structures sharded, A-step pair-sharded'},
             'roofline': {'bound': 'hbm', 'kernel': 'anneal_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'traffic_source': traffic_src,
                          'algorithmic_bytes_per_launch': float(np.mean(bytes_launch)),
                          'avg_launch_ms': a_ms},
             'cpu_baseline': cpu,
+            'asteps_DE': de,
             'breakdown': {'astep_ms': 1000 * float(np.mean(astep_s)), 'mstep_ms': 1000 * float(np.mean(mstep_s)),
                           'anneal_ms': a_ms, 'cg_ms': it.ctx.kernel_ms('cg'),
                           'actdist_ms': it.ctx.kernel_ms('actdist'), 'hic_select_ms': it.ctx.kernel_ms('hic_select'),
