@@ -32,6 +32,8 @@ IGM_MAX_ENVELOPES = 4
 IGM_ATOM_BEAD = 0x1
 IGM_ATOM_FIXED = 0x2
 IGM_ATOM_ENV0 = 0x10
+IGM_ENV_ELLIPSOID = 0
+IGM_ENV_VOLUME = 1
 
 # numpy views of the ABI structs (packed exactly like the C layouts)
 pair_dtype = np.dtype([('i', '<i4'), ('j', '<i4'), ('pwish', '<f8'), ('plast', '<f8')])
@@ -76,6 +78,18 @@ class MStepParams(ctypes.Structure):
         ('env_k', ctypes.c_double * IGM_MAX_ENVELOPES),
         ('neigh_capacity', ctypes.c_int32),
         ('flags', ctypes.c_int32),
+        ('env_kind', ctypes.c_int32 * IGM_MAX_ENVELOPES),
+    ]
+
+
+class VolumeMap(ctypes.Structure):
+    _fields_ = [
+        ('body_idx', ctypes.c_int32),
+        ('nvoxel', ctypes.c_int32 * 3),
+        ('center', ctypes.c_float * 3),
+        ('origin', ctypes.c_float * 3),
+        ('grid', ctypes.c_float * 3),
+        ('voxels', ctypes.c_void_p),
     ]
 
 
@@ -115,6 +129,7 @@ SIGNATURES = {
     'igm_hic_select': (_i32, [_vp, _u32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _f64, _f64,
                               _i32, _i32, _vp, _vp, _vp, ctypes.POINTER(_i64)]),
     'igm_population_transpose': (_i32, [_vp, _u32, _i32, _i32, _i32, _vp, _vp, _i32]),
+    'igm_mstep_set_volumes': (_i32, [_vp, _i32, _vp, _vp, _i32]),
     'igm_mstep_violations': (_i32, [_vp, _u32, ctypes.POINTER(MStepParams), _i32, _i32, _vp, _vp, _vp,
                                     _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _f64, _vp]),
 }

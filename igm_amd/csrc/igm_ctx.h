@@ -20,6 +20,9 @@ struct igm_ctx {
     std::map<std::string, std::pair<void*, size_t>> ws;
     // per kernel family: (start, stop) events of its last launch on `stream`
     std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> kev;
+    // volumetric maps staged by igm_mstep_set_volumes (device copies live in ws slots
+    // "vol_maps", "vol_vox", "vol_smap")
+    int vol_nmap = 0, vol_nsmap = 0;
     int num_cus = 256;
     size_t lds_per_block = 65536;
 };

@@ -448,7 +448,7 @@ __device__ __noinline__ void pair_walk(int a, T xi, T yi, T zi, T ri, const vec4
 // Total force on atom a, gathered by its owner thread: pairs from the Verlet
 // list (or the cell walk around the build-time position b*), bonds B, envelopes.
 template <typename T, bool EN, typename OffT>
-__device__ __forceinline__ void atom_force(int a, const vec4_t<T>& p0, uint32_t fl, const vec4_t<T>* pos,
+__device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, uint32_t fl, const vec4_t<T>* pos,
                                            const NList<T, OffT>& L, T bx, T by, T bz, const BondView& B,
                                            const DevParams& P, T evf, T envf, T& fx, T& fy,
                                            T& fz, double& ep, double& eb, double (&ee)[IGM_MAX_ENVELOPES]) {
@@ -562,7 +562,10 @@ __device__ __forceinline__ void atom_force(int a, const vec4_t<T>& p0, uint32_t 
     for (int e = 0; e < P.nenv; ++e) {
         if (!(fl & (IGM_ATOM_ENV0 << e))) continue;
         double en = 0.0;
-        if constexpr (std::is_same<T, float>::value)
+        if (P.env_kind[e] == IGM_ENV_VOLUME) {
+            const T kk = std::is_same<T, float>::value ? (T)P.env_k[e] : (T)P.env_k_d[e];
+            volume_term<T, EN>(xi, yi, zi, P.vmaps[P.vsmap ? P.vsmap[s] : 0], P.vvox, envf, kk, fx, fy, fz, en);
+        } else if constexpr (std::is_same<T, float>::value)
             envelope_term<T, EN>(xi, yi, zi, rad, P.env_abc[e][0] * envf, P.env_abc[e][1] * envf,
                                  P.env_abc[e][2] * envf, P.env_k[e], fx, fy, fz, en);
         else
@@ -775,7 +778,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                         const BondView B = lds_bonds ? BondView{nullptr, nullptr, sm.rest + sm.boff[a], sm.btab,
                                                                 (int)sm.boff[a + 1] - (int)sm.boff[a]}
                                                      : BondView{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
-                        atom_force<float, false, uint16_t>(a, sm.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], sm.pos, sm.L,
+                        atom_force<float, false, uint16_t>(s, a, sm.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], sm.pos, sm.L,
                                                            pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
                                                            pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz, ep,
                                                            eb, ee);
@@ -1142,7 +1145,7 @@ __global__ void __launch_bounds__(kPopBS) pop_forces_kernel(PopArgs A, float evf
     const float4 b = A.xb4[i];
     double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
     float fx, fy, fz;
-    atom_force<float, false, int>(a, W.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], W.pos, L, b.x, b.y, b.z, B, A.P, evf, envf, fx, fy,
+    atom_force<float, false, int>(s, a, W.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], W.pos, L, b.x, b.y, b.z, B, A.P, evf, envf, fx, fy,
                                   fz, ep, eb, ee);
     A.f4[i] = make_float4(fx, fy, fz, 0.f);
 }
@@ -1393,7 +1396,7 @@ __global__ void __launch_bounds__(NT) cg_kernel(CGArgs A) {
                 double e_e[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
                 double fx, fy, fz;
                 const BondView B{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
-                atom_force<double, true, int>(a, pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], pos, L, XB[a], XB[ldn + a],
+                atom_force<double, true, int>(s, a, pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], pos, L, XB[a], XB[ldn + a],
                                               XB[2 * ldn + a], B, A.P, A.evf, A.envf, fx, fy, fz, vv[0], vv[1], e_e);
                 for (int e = 0; e < IGM_MAX_ENVELOPES; ++e) vv[2 + e] += e_e[e];
                 F[a] = fx;
@@ -1837,6 +1840,24 @@ int make_devparams(igm_ctx* c, const igm_mstep_params* prm, int natom, const flo
         }
         P->env_k[e] = (float)prm->env_k[e];
         P->env_k_d[e] = prm->env_k[e];
+        P->env_kind[e] = prm->env_kind[e];
+        if (P->env_kind[e] != IGM_ENV_ELLIPSOID && P->env_kind[e] != IGM_ENV_VOLUME)
+            return fail(c, IGM_E_INVALID, "env_kind[%d] = %d", e, P->env_kind[e]);
+        if (P->env_kind[e] == IGM_ENV_VOLUME) {
+            if (c->vol_nmap <= 0)
+                return fail(c, IGM_E_INVALID, "envelope %d is volumetric but no map was staged (igm_mstep_set_volumes)",
+                            e);
+            void *pm, *pv, *ps;
+            IGM_TRY(workspace(c, "vol_maps", 1, &pm));
+            IGM_TRY(workspace(c, "vol_vox", 1, &pv));
+            P->vmaps = (const VolMapDev*)pm;
+            P->vvox = (const int4*)pv;
+            P->vsmap = nullptr;
+            if (c->vol_nsmap > 0) {
+                IGM_TRY(workspace(c, "vol_smap", 1, &ps));
+                P->vsmap = (const int*)ps;
+            }
+        }
     }
     // Verlet skin: LAMMPS 'neighbor maxrad bin' uses skin = maxrad.  The skin only sets
     // how often the (always complete) list is rebuilt, not the forces; 0.7 maxrad is the
@@ -1915,11 +1936,70 @@ bool lds_fits(int natom, LaunchCfg* cfg) {
     return false;
 }
 
+// ------------------------------------------------------------- volume maps
+int set_volumes(igm_ctx* c, int32_t nmap, const igm_volume_map* maps, const int32_t* struct_map, int32_t nstruct) {
+    if (nmap < 0 || (nmap > 0 && !maps) || (struct_map && nstruct <= 0))
+        return fail(c, IGM_E_INVALID, "igm_mstep_set_volumes: invalid arguments");
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    c->vol_nmap = 0;
+    c->vol_nsmap = 0;
+    if (nmap == 0) return IGM_OK;
+    std::vector<VolMapDev> hm(nmap);
+    long long tot = 0;
+    for (int m = 0; m < nmap; ++m) {
+        const igm_volume_map& v = maps[m];
+        if (!v.voxels || v.nvoxel[0] <= 0 || v.nvoxel[1] <= 0 || v.nvoxel[2] <= 0 || (v.body_idx != 0 && v.body_idx != 1))
+            return fail(c, IGM_E_INVALID, "igm_mstep_set_volumes: map %d malformed", m);
+        for (int d = 0; d < 3; ++d) {
+            if (!(v.grid[d] > 0.0f)) return fail(c, IGM_E_INVALID, "igm_mstep_set_volumes: map %d grid <= 0", m);
+            hm[m].n[d] = v.nvoxel[d];
+            hm[m].center[d] = v.center[d];
+            hm[m].origin[d] = v.origin[d];
+            hm[m].grid[d] = v.grid[d];
+        }
+        hm[m].body = v.body_idx;
+        hm[m].off = tot;
+        const long long nv = (long long)v.nvoxel[0] * v.nvoxel[1] * v.nvoxel[2];
+        for (long long q = 0; q < nv; ++q)
+            for (int d = 0; d < 3; ++d)
+                if (v.voxels[4 * q + d] < 0 || v.voxels[4 * q + d] >= v.nvoxel[d])
+                    return fail(c, IGM_E_INVALID, "igm_mstep_set_volumes: map %d voxel %lld: EDT index out of range",
+                                m, q);
+        tot += nv;
+    }
+    if (struct_map)
+        for (int s = 0; s < nstruct; ++s)
+            if (struct_map[s] < 0 || struct_map[s] >= nmap)
+                return fail(c, IGM_E_INVALID, "igm_mstep_set_volumes: struct_map[%d] = %d", s, struct_map[s]);
+    void *pm, *pv;
+    IGM_TRY(workspace(c, "vol_maps", sizeof(VolMapDev) * nmap, &pm));
+    IGM_TRY(workspace(c, "vol_vox", sizeof(int4) * (size_t)tot, &pv));
+    IGM_HIP_CHECK(c, hipMemcpyAsync(pm, hm.data(), sizeof(VolMapDev) * nmap, hipMemcpyHostToDevice, c->stream));
+    for (int m = 0; m < nmap; ++m) {
+        const long long nv = (long long)maps[m].nvoxel[0] * maps[m].nvoxel[1] * maps[m].nvoxel[2];
+        IGM_HIP_CHECK(c, hipMemcpyAsync((int4*)pv + hm[m].off, maps[m].voxels, sizeof(int4) * (size_t)nv,
+                                        hipMemcpyHostToDevice, c->stream));
+    }
+    if (struct_map) {
+        void* ps;
+        IGM_TRY(workspace(c, "vol_smap", sizeof(int) * nstruct, &ps));
+        IGM_HIP_CHECK(c, hipMemcpyAsync(ps, struct_map, sizeof(int) * nstruct, hipMemcpyHostToDevice, c->stream));
+        c->vol_nsmap = nstruct;
+    }
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    c->vol_nmap = nmap;
+    return IGM_OK;
+}
+
 // stage inputs + build the bond adjacency for all structures
 int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nstruct, int32_t natom,
             const float* radii, const uint32_t* atom_flags, const igm_bond* shared_bonds, int64_t nshared,
             const int64_t* sbond_ptr, const igm_bond* sbonds, Prepared* out) {
     if (natom <= 0 || natom > 65535) return fail(c, IGM_E_UNSUPPORTED, "natom=%d outside [1, 65535]", natom);
+    for (int e = 0; e < prm->nenvelopes && e < IGM_MAX_ENVELOPES; ++e)
+        if (prm->env_kind[e] == IGM_ENV_VOLUME && c->vol_nsmap > 0 && c->vol_nsmap < nstruct)
+            return fail(c, IGM_E_INVALID, "volume map index staged for %d structures, batch has %d", c->vol_nsmap,
+                        nstruct);
     const float* d_radii;
     const uint32_t* d_flags;
     const igm_bond* d_shared;
@@ -2478,6 +2558,12 @@ extern "C" int igm_velocity_create(igm_ctx* c, uint32_t flags, int32_t nseed, in
 
 /* Profiling aid (IGM_PROF=1 in the environment): cycle counters of the last LDS-path
  * anneal launch summed over structures: {build, force, rest, steps, builds}. */
+extern "C" int igm_mstep_set_volumes(igm_ctx* c, int32_t nmap, const igm_volume_map* maps,
+                                     const int32_t* struct_map, int32_t nstruct) {
+    if (!c) return IGM_E_INVALID;
+    return set_volumes(c, nmap, maps, struct_map, nstruct);
+}
+
 extern "C" int igm_mstep_last_profile(igm_ctx* c, unsigned long long* out) {
     if (!c || !out) return IGM_E_INVALID;
     auto it = c->ws.find("ms_prof");

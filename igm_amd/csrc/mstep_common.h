@@ -24,9 +24,21 @@ constexpr int kMaxWaves = 16;   // 1024 threads
 template <typename T>
 using vec4_t = typename std::conditional<std::is_same<T, float>::value, float4, double4>::type;
 
+// one volumetric map on the device (igm_volume_map; voxels at vvox + off)
+struct VolMapDev {
+    int n[3];
+    int body;
+    float center[3], origin[3], grid[3];
+    long long off;
+};
+
 // protocol constants shared by every structure of a launch
 struct DevParams {
     int nenv;
+    int env_kind[IGM_MAX_ENVELOPES];  // IGM_ENV_ELLIPSOID / IGM_ENV_VOLUME
+    const VolMapDev* vmaps;           // volume maps (igm_mstep_set_volumes)
+    const int4* vvox;
+    const int* vsmap;                 // map of structure s (NULL: map 0)
     float env_abc[IGM_MAX_ENVELOPES][3];
     float env_k[IGM_MAX_ENVELOPES];
     double env_abc_d[IGM_MAX_ENVELOPES][3];
@@ -203,6 +215,34 @@ __device__ __forceinline__ void envelope_term(T x, T y, T z, T rad, T a, T b, T 
     fy -= ka * t * (A * y + B * y * iy);
     fz -= ka * t * (A * z + B * z * iz);
     if (EN) e += 0.5 * (double)ka * (double)t * (double)t;
+}
+
+// volumetric map restraint (IGM_ENV_VOLUME; form documented in igm_hip.h): pulls a
+// member atom whose voxel violates the map to its nearest lamina voxel centre
+template <typename T, bool EN>
+__device__ __forceinline__ void volume_term(T x, T y, T z, const VolMapDev& m, const int4* __restrict__ vox,
+                                            T envf, T k, T& fx, T& fy, T& fz, double& e) {
+    const T p[3] = {x, y, z};
+    T o[3], g[3];
+    int v[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        o[d] = (T)m.origin[d] * envf;
+        g[d] = (T)m.grid[d] * envf;
+        int iv = (int)rint((p[d] - o[d]) / g[d]);
+        iv = iv < 0 ? 0 : (iv >= m.n[d] ? m.n[d] - 1 : iv);
+        v[d] = iv;
+    }
+    const int4 r = vox[m.off + ((long long)v[0] * m.n[1] + v[1]) * m.n[2] + v[2]];
+    const bool outside_ok = (m.body == 0) == (k > T(0));  // violation = outside (else inside)
+    const bool viol = outside_ok ? (r.w == 0) : (r.w != 0);
+    if (!viol) return;
+    const T dx = x - (o[0] + g[0] * (T)r.x), dy = y - (o[1] + g[1] * (T)r.y), dz = z - (o[2] + g[2] * (T)r.z);
+    const T ka = fabs(k);
+    fx -= ka * dx;
+    fy -= ka * dy;
+    fz -= ka * dz;
+    if (EN) e += 0.5 * (double)ka * ((double)dx * dx + (double)dy * dy + (double)dz * dz);
 }
 
 }  // namespace ms

@@ -6,6 +6,7 @@
 // histogram bins and the (ratio > tol) counts match the reference exactly.
 #include "exact_math.h"
 #include "igm_ctx.h"
+#include "mstep_common.h"
 
 namespace {
 
@@ -52,10 +53,48 @@ struct VArgs {
     double class_cr[kMaxClass];
     double env_abc[IGM_MAX_ENVELOPES][3];
     double env_k[IGM_MAX_ENVELOPES];
-    double env_scale[IGM_MAX_ENVELOPES];
+    double env_scale[IGM_MAX_ENVELOPES];  // ellipsoid: violation scale; volume: contact_range
+    int env_kind[IGM_MAX_ENVELOPES];
+    const igm::ms::VolMapDev* vmaps;       // volume maps (igm_mstep_set_volumes)
+    const int4* vvox;
+    const int* vsmap;
     double tol;
     int64_t* stats;
 };
+
+// ExpEnvelope.getScores (igm/model/forces.py:306-417) of one particle, restated with its
+// NumPy semantics: f32 position minus float64 origin over float64 grid, round half to
+// even, -1 outside the grid; the reference's inside-grid test `id_int.all() >= 0` is
+// always true, so a -1 index reads the last voxel (Python negative indexing) and the
+// score uses the -1 itself.
+__device__ double volume_score(const float* p, const igm::ms::VolMapDev& m, const int4* vox, double k, double cr) {
+    double o[3], g[3];
+    int id[3], w[3];
+    for (int d = 0; d < 3; ++d) {
+        o[d] = (double)m.origin[d];
+        g[d] = (double)m.grid[d];
+        if (m.body == 0 && k < 0.0) {
+            o[d] = o[d] * cr;
+            g[d] = g[d] * cr;
+        }
+        if (m.body == 1 && k < 0.0) {
+            o[d] = o[d] / cr;
+            g[d] = g[d] / cr;
+        }
+        const double ix = ((double)p[d] - o[d]) / g[d];
+        id[d] = (ix < 0.0 || ix >= (double)m.n[d]) ? -1 : (int)rint(ix);
+        if (id[d] >= m.n[d]) id[d] = m.n[d] - 1;  // the reference raises IndexError here
+        w[d] = id[d] < 0 ? m.n[d] - 1 : id[d];
+    }
+    const int4 r = vox[m.off + ((long long)w[0] * m.n[1] + w[1]) * m.n[2] + w[2]];
+    const bool cond = (m.body == 0) ? ((r.w == 0 && k > 0.0) || (r.w != 0 && k < 0.0))
+                                    : ((r.w != 0 && k > 0.0) || (r.w == 0 && k < 0.0));
+    if (!cond) return 0.0;
+    const double v0 = g[0] * (double)(r.x - id[0]), v1 = g[1] * (double)(r.y - id[1]),
+                 v2 = g[2] * (double)(r.z - id[2]);
+    // np.linalg.norm = sqrt(ddot): the reference BLAS sums (x0^2 + x2^2) + x1^2
+    return igm::sqrt_rn((v0 * v0 + v2 * v2) + v1 * v1) / igm::sqrt_rn((g[0] * g[0] + g[2] * g[2]) + g[1] * g[1]);
+}
 
 __global__ void __launch_bounds__(256) violations_kernel(VArgs A) {
     __shared__ int h[kMaxClass * kRec];
@@ -92,6 +131,11 @@ __global__ void __launch_bounds__(256) violations_kernel(VArgs A) {
         for (int a = t; a < A.natom; a += 256) {
             if (!(A.aflags[(size_t)s * A.afs + a] & (IGM_ATOM_ENV0 << e))) continue;
             const float* p = x + 3 * a;
+            if (A.env_kind[e] == IGM_ENV_VOLUME) {
+                record(he, volume_score(p, A.vmaps[A.vsmap ? A.vsmap[s] : 0], A.vvox, A.env_k[e], A.env_scale[e]),
+                       A.tol);
+                continue;
+            }
             const double r = (double)A.radii[a];
             double acc = 0.0;
             for (int d = 0; d < 3; ++d) {
@@ -142,6 +186,23 @@ extern "C" int igm_mstep_violations(igm_ctx* c, uint32_t flags, const igm_mstep_
         A.env_k[e] = prm->env_k[e];
         A.env_scale[e] = env_scale ? env_scale[e] : 0.1 * (prm->env_semiaxes[e][0] + prm->env_semiaxes[e][1] +
                                                              prm->env_semiaxes[e][2]) / 3.0;
+        A.env_kind[e] = prm->env_kind[e];
+        if (A.env_kind[e] == IGM_ENV_VOLUME) {
+            if (!env_scale) A.env_scale[e] = 0.95;  // GenEnvelope's contact_range (genenvelope.py:48-58)
+            if (c->vol_nmap <= 0) return fail(c, IGM_E_INVALID, "igm_mstep_violations: no volume map staged");
+            if (c->vol_nsmap > 0 && c->vol_nsmap < nstruct)
+                return fail(c, IGM_E_INVALID, "igm_mstep_violations: volume map index staged for %d structures",
+                            c->vol_nsmap);
+            void *pm, *pv, *ps;
+            IGM_TRY(workspace(c, "vol_maps", 1, &pm));
+            IGM_TRY(workspace(c, "vol_vox", 1, &pv));
+            A.vmaps = (const igm::ms::VolMapDev*)pm;
+            A.vvox = (const int4*)pv;
+            if (c->vol_nsmap > 0) {
+                IGM_TRY(workspace(c, "vol_smap", 1, &ps));
+                A.vsmap = (const int*)ps;
+            }
+        }
     }
     int64_t nsb = 0;
     if (sbond_ptr) {

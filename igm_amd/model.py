@@ -17,7 +17,7 @@ as flat arrays shared by the whole population:
 """
 import numpy as np
 
-from ._lib import (IGM_ATOM_BEAD, IGM_ATOM_ENV0, IGM_ATOM_FIXED, IGM_MAX_ENVELOPES, IGM_MAX_STAGES,
+from ._lib import (IGM_ATOM_BEAD, IGM_ATOM_ENV0, IGM_ATOM_FIXED, IGM_ENV_VOLUME, IGM_MAX_ENVELOPES, IGM_MAX_STAGES,
                    LOWER_BOUND_BIT, MStepParams, bond_dtype)
 
 # restraint classes used for violation statistics (ModelingStep.py:511-557)
@@ -134,8 +134,13 @@ def params_from_cfg(cfg, envelopes, evfactor=1.0, skin=None):
         raise ValueError('at most %d envelopes' % IGM_MAX_ENVELOPES)
     p.nenvelopes = len(envelopes)
     for e, (abc, k) in enumerate(envelopes):
-        for d in range(3):
-            p.env_semiaxes[e][d] = float(abc[d])
+        if isinstance(abc, str):  # ('volume', k): fix volumetricrestraint (lammps.py:305-310)
+            if abc != 'volume':
+                raise ValueError('unknown envelope kind %r' % abc)
+            p.env_kind[e] = IGM_ENV_VOLUME
+        else:
+            for d in range(3):
+                p.env_semiaxes[e][d] = float(abc[d])
         p.env_k[e] = float(k)
     p.neigh_capacity = 0
     return p
@@ -182,7 +187,7 @@ def from_igm_model(model):
       DUMMY_DYNAMIC -> mobile centroid without pair interactions;
       HARMONIC_UPPER/LOWER_BOUND -> bonds in force order; EXCLUDED_VOLUME -> evfactor;
       ENVELOPE -> envelope (only those with particles get a LAMMPS group, lammps.py:231-233).
-    Volumetric (exp_map) envelopes are out of scope and raise NotImplementedError."""
+    ExpEnvelope (exp_map) -> ('volume', k) envelope; its map file in lm.volume_files."""
     radii, flags, xyz, imap = [], [], [], []
     for p in model.particles:
         pos = np.asarray(p.pos, np.float32)
@@ -207,16 +212,22 @@ def from_igm_model(model):
     flags = np.asarray(flags, np.uint32)
     imap = np.asarray(imap, np.int64)
     bi, bj, br, bk, lower, envelopes, evfactor = [], [], [], [], [], [], 1.0
+    volume_files = []
     for f in model.forces:
         if f.ftype in (_ENVELOPE, _GENERAL_ENVELOPE):
-            if getattr(f, 'shape', 'ellipsoid') != 'ellipsoid':
-                raise NotImplementedError('envelope shape %s (volumetric maps are out of scope)' % f.shape)
+            shape = getattr(f, 'shape', 'ellipsoid')
+            if shape not in ('ellipsoid', 'exp_map'):
+                raise NotImplementedError('Envelope (%s) not implemented' % shape)  # lammps.py:313-315
             if len(f.particle_ids):
                 e = len(envelopes)
                 if e >= IGM_MAX_ENVELOPES:
                     raise ValueError('at most %d envelopes' % IGM_MAX_ENVELOPES)
                 flags[imap[np.asarray(f.particle_ids, np.int64)]] |= np.uint32(IGM_ATOM_ENV0 << e)
-                envelopes.append((tuple(float(v) for v in f.semiaxes), float(f.k)))
+                if shape == 'exp_map':  # ExpEnvelope -> fix volumetricrestraint (lammps.py:305-310)
+                    envelopes.append(('volume', float(f.k)))
+                    volume_files.append(f.volume_file)
+                else:
+                    envelopes.append((tuple(float(v) for v in f.semiaxes), float(f.k)))
         elif f.ftype == _EXCLUDED_VOLUME:
             evfactor = float(f.k)
         elif f.ftype in (_UPPER, _LOWER):
@@ -233,5 +244,7 @@ def from_igm_model(model):
         bonds['j'] = np.asarray(bj, np.uint32) | np.where(lower, LOWER_BOUND_BIT, np.uint32(0)).astype(np.uint32)
         bonds['r0'] = br
         bonds['k'] = bk
-    return LammpsLikeModel(np.asarray(radii, np.float32), flags, np.stack(xyz).astype(np.float32), bonds,
-                           envelopes, evfactor, imap, getattr(model, 'id', 0))
+    lm = LammpsLikeModel(np.asarray(radii, np.float32), flags, np.stack(xyz).astype(np.float32), bonds,
+                         envelopes, evfactor, imap, getattr(model, 'id', 0))
+    lm.volume_files = volume_files
+    return lm

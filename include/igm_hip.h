@@ -174,6 +174,31 @@ int igm_damid_select(igm_ctx* ctx, uint32_t flags, int32_t nstruct, int32_t nato
                      const double* semiaxes, double contact_range, uint32_t env_bit,
                      const uint32_t* base_flags, uint32_t* out_flags, int32_t* n_selected);
 
+/* Volumetric nuclear-body maps (VolumeFile .bin, igm/utils/files.py:137-166): header
+ * int32 body_idx (0 nucleus, 1 nucleolus), int32[3] nvoxel, f32[3] center, origin, grid,
+ * then int32 [nx][ny][nz][4] = (nearest-lamina voxel i, j, k, inside flag).
+ * The LAMMPS fix's force form is not in the reference (lammpgen is external, SURVEY
+ * M7d: parity unpinned).  Implemented form, per member atom of a volume envelope:
+ *   v = round((x - envf*origin) / (envf*grid)) clamped to the grid; if the voxel
+ *   violates the restraint (nucleus, k>0: outside; nucleolus, k>0: inside; k<0: the
+ *   opposite, as ExpEnvelope.getScores, forces.py:306-417) the atom is pulled to the
+ *   centre of its nearest lamina voxel p = envf*(origin + grid*edt(v)):
+ *   E = |k|/2 |x - p|^2, F = -|k| (x - p).
+ * Violation scores restate ExpEnvelope.getScores exactly (contact_range 0.95 geometry
+ * shrink for k<0, its index quirks included). */
+typedef struct {
+    int32_t body_idx;
+    int32_t nvoxel[3];
+    float center[3], origin[3], grid[3];
+    const int32_t* voxels; /* host pointer: nx*ny*nz*4 int32 */
+} igm_volume_map;
+
+/* Stage maps in the context for later igm_mstep_* calls: struct_map[s] selects the
+ * map of structure s of a batch (volumes_idx[sid % len], ModelingStep.py:265-270);
+ * NULL = map 0 for every structure.  nmap = 0 clears. */
+int igm_mstep_set_volumes(igm_ctx* ctx, int32_t nmap, const igm_volume_map* maps,
+                          const int32_t* struct_map, int32_t nstruct);
+
 /* ---- M-step ---------------------------------------------------------------
  * Batched replacement of lammps.optimize (lammps.py:361-492): the protocol of
  * create_lammps_script (lammps.py:149-358) -- per stage: fix adapt of the soft
@@ -210,7 +235,13 @@ typedef struct {
     int32_t neigh_capacity; /* HBM neighbour-list budget, mean entries per atom (0 = 64); atoms past
                                the budget take their pair forces from a walk of the build-time cell grid */
     int32_t flags;          /* IGM_MSTEP_* below                        */
+    int32_t env_kind[IGM_MAX_ENVELOPES]; /* IGM_ENV_ELLIPSOID (0) or IGM_ENV_VOLUME (1)  */
 } igm_mstep_params;
+
+/* envelope kinds (igm_mstep_params.env_kind) */
+#define IGM_ENV_ELLIPSOID 0 /* fix ellipsoidalenvelope a b c k (lammps.py:292-303)              */
+#define IGM_ENV_VOLUME 1    /* fix volumetricrestraint file envf k (lammps.py:305-310) with the
+                               map of igm_mstep_set_volumes; env_semiaxes unused */
 
 /* igm_mstep_params.flags */
 #define IGM_MSTEP_FORCE_GLOBAL 0x1 /* use the HBM-resident kernels even when a structure fits in LDS */

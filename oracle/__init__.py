@@ -106,6 +106,28 @@ def mstep_run(params, xyz, radii, flags, shared, sptr, sbonds, seeds, nthreads=1
     return xyz, info, x64
 
 
+_vol_keep = []
+
+
+def set_volume(vol):
+    """The map used by IGM_ENV_VOLUME envelopes in later oracle calls (None clears).
+    vol: dict(body_idx, nvoxel, origin, grid, matrice (nx, ny, nz, 4) int32)."""
+    import ctypes as C
+    L = lib()
+    L.oracle_set_volume.restype = C.c_int
+    L.oracle_set_volume.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    del _vol_keep[:]
+    if vol is None:
+        L.oracle_set_volume(0, None, None, None, None)
+        return
+    n = np.ascontiguousarray(vol['nvoxel'], np.int32)
+    o = np.ascontiguousarray(vol['origin'], np.float32)
+    g = np.ascontiguousarray(vol['grid'], np.float32)
+    m = np.ascontiguousarray(vol['matrice'], np.int32)
+    _vol_keep.extend([n, o, g, m])
+    L.oracle_set_volume(int(vol['body_idx']), n.ctypes.data, o.ctypes.data, g.ctypes.data, m.ctypes.data)
+
+
 def mstep_forces(params, xyz, radii, flags, shared, sptr, sbonds, evf, envf):
     import ctypes as C
     xyz = np.ascontiguousarray(xyz, np.float32)

@@ -233,6 +233,49 @@ static double envelope_atom(const model_t* m, int e, int i, double* fx, double* 
     return 0.5 * ka * t * t;
 }
 
+/* the volumetric map of IGM_ENV_VOLUME envelopes (one map for the whole call; the
+ * form documented in include/igm_hip.h: pull a violating atom to the centre of its
+ * voxel's nearest lamina voxel, E = |k|/2 d^2) */
+static struct {
+    int on, body, n[3];
+    float origin[3], grid[3];
+    const int32_t* vox;
+} g_vol;
+
+int oracle_set_volume(int body, const int32_t* n, const float* origin, const float* grid, const int32_t* vox) {
+    g_vol.on = vox != NULL;
+    g_vol.body = body;
+    for (int d = 0; d < 3; ++d) {
+        g_vol.n[d] = n ? n[d] : 0;
+        g_vol.origin[d] = origin ? origin[d] : 0.0f;
+        g_vol.grid[d] = grid ? grid[d] : 1.0f;
+    }
+    g_vol.vox = vox;
+    return 0;
+}
+
+static double volume_atom(const model_t* m, int e, int i, double* fx, double* fy, double* fz) {
+    const double k = m->prm->env_k[e];
+    double o[3], g[3], t[3];
+    int v[3];
+    for (int d = 0; d < 3; ++d) {
+        o[d] = (double)g_vol.origin[d] * m->envf;
+        g[d] = (double)g_vol.grid[d] * m->envf;
+        int iv = (int)rint((m->x[3 * i + d] - o[d]) / g[d]);
+        v[d] = iv < 0 ? 0 : (iv >= g_vol.n[d] ? g_vol.n[d] - 1 : iv);
+    }
+    const int32_t* r = g_vol.vox + 4 * (((long)v[0] * g_vol.n[1] + v[1]) * g_vol.n[2] + v[2]);
+    const int outside_ok = (g_vol.body == 0) == (k > 0);
+    const int viol = outside_ok ? (r[3] == 0) : (r[3] != 0);
+    if (!viol) return 0.0;
+    for (int d = 0; d < 3; ++d) t[d] = m->x[3 * i + d] - (o[d] + g[d] * (double)r[d]);
+    const double ka = fabs(k);
+    *fx = -ka * t[0];
+    *fy = -ka * t[1];
+    *fz = -ka * t[2];
+    return 0.5 * ka * (t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+}
+
 static double energy_force(model_t* m) {
     check_neighbors(m);
     const int n = m->n;
@@ -288,7 +331,12 @@ static double energy_force(model_t* m) {
         for (int i = 0; i < n; ++i) {
             if (!(m->fl[i] & (IGM_ATOM_ENV0 << e))) continue;
             double fx = 0, fy = 0, fz = 0;
-            ee += envelope_atom(m, e, i, &fx, &fy, &fz);
+            if (m->prm->env_kind[e] == IGM_ENV_VOLUME) {
+                if (!g_vol.on) continue;
+                ee += volume_atom(m, e, i, &fx, &fy, &fz);
+            } else {
+                ee += envelope_atom(m, e, i, &fx, &fy, &fz);
+            }
             f[3 * i] += fx;
             f[3 * i + 1] += fy;
             f[3 * i + 2] += fz;
