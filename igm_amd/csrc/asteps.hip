@@ -21,6 +21,7 @@
 
 #include "exact_math.h"
 #include "igm_ctx.h"
+#include "mstep_common.h"
 
 namespace {
 using namespace igm;
@@ -189,6 +190,137 @@ __global__ void __launch_bounds__(kBT) damid_kernel(DamidArgs A) {
         if (threadIdx.x == 0) A.res[q].ad = ad;
     }
     // rows (i, ad, p) for i in ii (py:473) through '%.5f' and genfromtxt(float32)
+    const float dist = (float)round_dec(ad, 1e5);
+    const float prob = (float)round_dec(sh_p, 1e5);
+    const int64_t base = A.rowoff[q];
+    for (int ci = threadIdx.x; ci < nc; ci += kBT) {
+        igm_damid_row w;
+        w.loc = A.cidx[c0 + ci];
+        w.dist = dist;
+        w.prob = prob;
+        A.rows[base + ci] = w;
+    }
+}
+
+// ---------------------------------------------------------------- DamID, exp_map
+// get_damid_actdist_exp (DamidActivationDistanceStep.py:475-577) with snormsq_exp
+// (:79-115): the squared distance of a bead to its voxel's nearest lamina voxel
+// (inside the grid) or, outside, |(voxel - center) * grid|^2 in the reference's mixed
+// units; all float64 (f32 coordinate minus float64 map geometry), np.round half to
+// even, np.dot summing (t0^2 + t2^2) + t1^2 like the reference BLAS.  Distances are
+// sorted ASCENDING here (d_sq.sort(axis=1)); pnow counts d_sq >= contact_range.
+struct DamidExpArgs {
+    const float* xyz;
+    int S;
+    const int* cptr;
+    const int* cidx;
+    const int* loci;
+    const float* pexp;
+    const float* plast;
+    int nloci;
+    int it_corr;
+    double cr;
+    const igm::ms::VolMapDev* maps;
+    const int4* vox;
+    const int* smap;  // (S) map of each structure
+    igm_pair_result* res;
+    const int64_t* rowoff;
+    igm_damid_row* rows;
+};
+
+__device__ __forceinline__ double damid_exp_key(const DamidExpArgs& A, int bead, int s) {
+    const igm::ms::VolMapDev m = A.maps[A.smap[s]];
+    float p[3];
+    load3(A.xyz, A.S, bead, s, p[0], p[1], p[2]);
+    long long v[3];
+    bool in = true;
+    for (int d = 0; d < 3; ++d) {
+        v[d] = (long long)rint(((double)p[d] - (double)m.origin[d]) / (double)m.grid[d]);
+        in = in && v[d] >= 0 && v[d] < m.n[d];
+    }
+    double t[3];
+    if (in) {
+        const int4 r = A.vox[m.off + (v[0] * m.n[1] + v[1]) * m.n[2] + v[2]];
+        const int e[3] = {r.x, r.y, r.z};
+        for (int d = 0; d < 3; ++d) t[d] = (double)p[d] - ((double)e[d] * (double)m.grid[d] + (double)m.origin[d]);
+    } else {
+        for (int d = 0; d < 3; ++d) t[d] = ((double)v[d] - (double)m.center[d]) * (double)m.grid[d];
+    }
+    return (t[0] * t[0] + t[2] * t[2]) + t[1] * t[1];
+}
+
+__global__ void __launch_bounds__(kBT) damid_exp_kernel(DamidExpArgs A) {
+    const int q = blockIdx.x;
+    if (q >= A.nloci) return;
+    __shared__ int sh_red[kBT / 64];
+    __shared__ unsigned hist[256];
+    __shared__ long long sh_m;
+    __shared__ unsigned long long sh_prefix, sh_mask;
+    __shared__ double sh_p;
+    __shared__ int sh_o;
+    const int I = A.loci[q];
+    const int c0 = A.cptr[I], nc = A.cptr[I + 1] - c0;
+    const int S = A.S;
+    int cnt = 0;
+    for (int ci = 0; ci < nc; ++ci) {
+        const int bead = A.cidx[c0 + ci];
+        for (int s = threadIdx.x; s < S; s += kBT) cnt += damid_exp_key(A, bead, s) >= A.cr;
+    }
+    cnt = block_sum(cnt, sh_red);
+    const int64_t nS = (int64_t)nc * S;
+    if (threadIdx.x == 0) {
+        const double pnow = nS > 0 ? (double)cnt / (double)nS : 0.0;
+        const double pexp = (double)A.pexp[q];
+        const double p = (A.it_corr == 1) ? damid_clean(pexp, damid_clean(pnow, (double)A.plast[q])) : pexp;
+        int o = -1;
+        if (p > 0.0 && nS > 0) {
+            const double ox = rint((double)nS * p);
+            o = (ox >= (double)(nS - 1)) ? (int)(nS - 1) : (int)ox;
+        }
+        sh_p = p;
+        sh_o = o;
+        sh_m = o;  // ascending: the o-th smallest
+        sh_prefix = 0ull;
+        sh_mask = 0ull;
+        igm_pair_result r;
+        r.p = p;
+        r.pnow = pnow;
+        r.o = o;
+        r.nrows = nc;
+        r.ad = __longlong_as_double(0x7ff8000000000000LL);
+        A.res[q] = r;
+    }
+    __syncthreads();
+    double ad = 1e-9;  // py:540
+    if (sh_o >= 0) {
+        for (int shift = 56; shift >= 0; shift -= 8) {
+            hist[threadIdx.x] = 0u;
+            __syncthreads();
+            const unsigned long long prefix = sh_prefix, mask = sh_mask;
+            for (int ci = 0; ci < nc; ++ci) {
+                const int bead = A.cidx[c0 + ci];
+                for (int s = threadIdx.x; s < S; s += kBT) {
+                    const unsigned long long u = (unsigned long long)__double_as_longlong(damid_exp_key(A, bead, s));
+                    if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255ull], 1u);
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                long long m = sh_m;
+                int b = 0;
+                for (; b < 255; ++b) {
+                    if (m < (long long)hist[b]) break;
+                    m -= hist[b];
+                }
+                sh_m = m;
+                sh_prefix = prefix | ((unsigned long long)b << shift);
+                sh_mask = mask | (255ull << shift);
+            }
+            __syncthreads();
+        }
+        ad = sqrt_rn(__longlong_as_double((long long)sh_prefix));
+        if (threadIdx.x == 0) A.res[q].ad = ad;
+    }
     const float dist = (float)round_dec(ad, 1e5);
     const float prob = (float)round_dec(sh_p, 1e5);
     const int64_t base = A.rowoff[q];
@@ -470,8 +602,13 @@ extern "C" int igm_damid_actdist(igm_ctx* c, uint32_t flags, const float* xyz, i
                                  int64_t* nrows_out) {
     if (!c) return IGM_E_INVALID;
     if (nbead <= 0 || nstruct <= 0 || nhap <= 0 || nloci < 0 || !xyz || !radii || !copy_ptr || !copy_idx ||
-        (nloci > 0 && (!loci || !p_exp || !plast)) || !nrows_out || !nucleus_param || (shape != 0 && shape != 1))
+        (nloci > 0 && (!loci || !p_exp || !plast)) || !nrows_out || (shape < 0 || shape > IGM_DAMID_EXP_MAP) ||
+        (shape != IGM_DAMID_EXP_MAP && !nucleus_param))
         return fail(c, IGM_E_INVALID, "igm_damid_actdist: invalid arguments");
+    if (shape == IGM_DAMID_EXP_MAP && (c->vol_nmap <= 0 || (c->vol_nsmap > 0 && c->vol_nsmap != nstruct)))
+        return fail(c, IGM_E_INVALID,
+                    "igm_damid_actdist: exp_map needs maps staged by igm_mstep_set_volumes with one map index per "
+                    "structure (%d staged, %d structures)", c->vol_nsmap, nstruct);
     IGM_HIP_CHECK(c, hipSetDevice(c->device));
     *nrows_out = 0;
     if (nloci == 0) return IGM_OK;
@@ -531,6 +668,42 @@ extern "C" int igm_damid_actdist(igm_ctx* c, uint32_t flags, const float* xyz, i
     }
     igm_damid_row* d_rows;
     IGM_TRY(out_device(c, flags, "dm_rows", rows, (size_t)total, &d_rows));
+    if (shape == IGM_DAMID_EXP_MAP) {
+        DamidExpArgs E;
+        E.xyz = d_xyz;
+        E.S = nstruct;
+        E.cptr = d_cptr;
+        E.cidx = d_cidx;
+        E.loci = d_loci;
+        E.pexp = d_pexp;
+        E.plast = d_plast;
+        E.nloci = nloci;
+        E.it_corr = it_corr;
+        E.cr = contact_range;
+        void *pm, *pv, *ps;
+        IGM_TRY(workspace(c, "vol_maps", 1, &pm));
+        IGM_TRY(workspace(c, "vol_vox", 1, &pv));
+        E.maps = (const igm::ms::VolMapDev*)pm;
+        E.vox = (const int4*)pv;
+        if (c->vol_nsmap > 0) {
+            IGM_TRY(workspace(c, "vol_smap", 1, &ps));
+        } else {  // every structure uses map 0
+            IGM_TRY(workspace(c, "dm_smap0", sizeof(int) * nstruct, &ps));
+            IGM_HIP_CHECK(c, hipMemsetAsync(ps, 0, sizeof(int) * nstruct, c->stream));
+        }
+        E.smap = (const int*)ps;
+        E.res = d_res;
+        E.rowoff = d_off;
+        E.rows = d_rows;
+        {
+            Timed tm(c, "damid");
+            hipLaunchKernelGGL(damid_exp_kernel, dim3((unsigned)nloci), dim3(kBT), 0, c->stream, E);
+            IGM_HIP_CHECK(c, hipGetLastError());
+        }
+        IGM_TRY(to_host(c, flags, rows, d_rows, (size_t)total));
+        if (per_locus && !(flags & IGM_DEVICE_PTRS)) IGM_TRY(to_host(c, flags, per_locus, d_res, (size_t)nloci));
+        return finish(c, flags);
+    }
     DamidArgs A;
     A.xyz = d_xyz;
     A.S = nstruct;

@@ -23,7 +23,7 @@ from ._lib import damid_row_dtype, result_dtype
 
 damid_actdist_shape = [('loc', 'int32'), ('dist', 'float32'), ('prob', 'float32')]
 damid_actdist_fmt_str = "%6d %.5f %.5f"
-SHAPES = {'sphere': 0, 'ellipsoid': 1}
+SHAPES = {'sphere': 0, 'ellipsoid': 1, 'exp_map': 2}
 
 
 def select_loci(profile, sigma, last_rows=None):
@@ -42,6 +42,8 @@ def select_loci(profile, sigma, last_rows=None):
 def _nucleus_param(shape, nucleus_param):
     if shape not in SHAPES:
         raise NotImplementedError('DamID restraint for shape %s has not been implemented yet.' % shape)
+    if shape == 'exp_map':
+        return np.zeros(3, np.float64)
     if shape == 'sphere':
         return np.array([float(np.ravel(nucleus_param)[0])] * 3, np.float64)
     a = np.asarray(nucleus_param, np.float64).ravel()
@@ -51,10 +53,19 @@ def _nucleus_param(shape, nucleus_param):
 
 
 def compute_damid_actdist(xyz, radii, copy_ptr, copy_idx, loci, p_exp, plast, it_corr=1, contact_range=0.05,
-                          shape='sphere', nucleus_param=5000.0, device=0, return_per_locus=False, ctx=None):
+                          shape='sphere', nucleus_param=5000.0, device=0, return_per_locus=False, ctx=None,
+                          volumes=None, struct_map=None):
     """Rows of every selected locus, in locus order (the concatenation of all task()
-    batches).  xyz: (nbead, nstruct, 3) float32 bead-major (the .hss layout)."""
+    batches).  xyz: (nbead, nstruct, 3) float32 bead-major (the .hss layout).
+    shape 'exp_map' (get_damid_actdist_exp, py:475-577): `volumes` are the VolumeFile
+    maps (igm_amd.volume.read_volume) and struct_map[s] the map of structure s
+    (volumes_idx); they are staged into the context."""
     c = ctx or _lib.context(device)
+    if shape == 'exp_map':
+        from . import volume as V
+        if volumes is None:
+            raise ValueError('exp_map needs the volume maps')
+        V.stage(c, volumes, struct_map)
     xyz = np.ascontiguousarray(xyz, np.float32)
     assert xyz.ndim == 3 and xyz.shape[2] == 3, 'xyz must be (nbead, nstruct, 3)'
     radii = np.ascontiguousarray(radii, np.float32)

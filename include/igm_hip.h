@@ -110,6 +110,14 @@ int igm_astep_update_plast(igm_ctx* ctx, uint32_t flags, igm_pair* pairs, int64_
  * every locus, in locus order.  loci[q] is a haploid locus, p_exp[q]/plast[q] the
  * float32 values setup() stores (:199-217).  per_locus[q] (nullable) reports ad, p,
  * pnow, o (-1 when p <= 0: the dist is then 2) and nrows. */
+/* shape 2 = exp_map: get_damid_actdist_exp (:475-577) with snormsq_exp (:79-115) on the
+ * volumetric maps staged by igm_mstep_set_volumes (struct_map = the map of every
+ * structure, volumes_idx); distances ascending, pnow = count(d^2 >= contact_range),
+ * dist 1e-9 when p <= 0 (nucleus_param and radii unused). */
+#define IGM_DAMID_SPHERE 0
+#define IGM_DAMID_ELLIPSOID 1
+#define IGM_DAMID_EXP_MAP 2
+
 typedef struct {
     int32_t loc; /* diploid bead index                               */
     float dist;  /* damid_actdist.hdf5 {loc i4, dist f4, prob f4}    */

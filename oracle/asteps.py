@@ -178,3 +178,57 @@ def sprite_cluster_rg2(crd, hap_chrom, copy_ptr, copy_idx, cluster, reps, struct
 def keep_best(rg2s, k):
     """argpartition + argsort of SpriteAssignmentStep.task (py:138-139), ties by index."""
     return np.argsort(rg2s, kind='stable')[:k]
+
+
+def _snormsq_exp(x, vol):
+    """snormsq_exp (DamidActivationDistanceStep.py:79-115): float64 arithmetic on the
+    f32 coordinates, np.round half to even, np.dot as the reference BLAS sums it,
+    (t0^2 + t2^2) + t1^2."""
+    origin = np.array([float(v) for v in vol['origin']])
+    grid = np.array([float(v) for v in vol['grid']])
+    center = np.array([float(v) for v in vol['center']])
+    n = np.asarray(vol['nvoxel'])
+    mat = vol['matrice']
+    vox = np.round(np.array((np.asarray(x, np.float32) - origin) / grid)).astype(int)
+    out = []
+    for k in range(vox.shape[0]):
+        if (vox[k] >= 0).all() and (vox[k] < n).all():
+            t = x[k] - (mat[tuple(vox[k])][0:3] * grid + origin)
+        else:
+            t = (vox[k] - center) * grid
+        t = [float(v) for v in t]
+        out.append((t[0] * t[0] + t[2] * t[2]) + t[1] * t[1])
+    return out
+
+
+def damid_actdist_exp(crd, copy_ptr, copy_idx, loci, pexp, plast, it_corr, contact_range, maps, volumes_idx):
+    """get_damid_actdist_exp (py:475-577) + the text round trip: rows {loc, dist, prob}.
+    pexp/plast are per listed locus (the batch params); maps[m] is volume_idx m."""
+    S = crd.shape[1]
+    vidx = np.asarray(volumes_idx)
+    rows = []
+    for q, I in enumerate(loci):
+        ii = [int(v) for v in copy_idx[copy_ptr[I]:copy_ptr[I + 1]]]
+        nc = len(ii)
+        d = []
+        for m in sorted(set(vidx.tolist())):
+            where = np.where(vidx == m)[0]
+            for b in ii:
+                d += _snormsq_exp(crd[b][where], maps[m])
+        d = np.sort(np.array(d))
+        if it_corr == 1:
+            pnow = float(np.count_nonzero(d >= contact_range)) / (S * nc)
+            p = _clean(pexp[q], _clean(pnow, plast[q]))
+        else:
+            p = float(pexp[q])
+        ad = 1e-9
+        if p > 0:
+            o = min(nc * S - 1, int(np.round(np.float64(nc * S) * p)))
+            ad = float(np.sqrt(d[o]))
+        for i in ii:
+            a, b, c = ('%6d %.5f %.5f' % (i, ad, p)).split()
+            rows.append((int(a), f32(float(b)), f32(float(c))))
+    out = np.zeros(len(rows), [('loc', 'i4'), ('dist', 'f4'), ('prob', 'f4')])
+    if rows:
+        out['loc'], out['dist'], out['prob'] = zip(*rows)
+    return out

@@ -70,6 +70,51 @@ def main():
         out['b%d_pos' % body] = pos
     np.savez_compressed(os.path.join(HERE, 'volume_golden.npz'), **out)
     print('volume_golden.npz', os.path.getsize(os.path.join(HERE, 'volume_golden.npz')))
+    np.savez_compressed(os.path.join(HERE, 'damid_exp_golden.npz'), **make_damid_exp())
+    print('damid_exp_golden.npz', os.path.getsize(os.path.join(HERE, 'damid_exp_golden.npz')))
+
+
+def make_damid_exp():
+    """get_damid_actdist_exp (DamidActivationDistanceStep.py:475-577) on the demo
+    population with two nucleus maps (R 5500 and 5200, 100 nm grid) assigned
+    alternately through volumes_idx (one entry per structure), it_corr 0/1, after the
+    '%6d %.5f %.5f' text round trip.  Only two-copy loci: a batch that mixes copy
+    counts makes the reference's np.array(d_sq).sort(axis=1) fail."""
+    damid_mod = importlib.import_module('igm.steps.DamidActivationDistanceStep')
+    d = np.load(os.path.join(HERE, 'demo_population.npz'))
+    ptr, idx = d['copy_ptr'], d['copy_idx']
+    copy_index = {h: [int(x) for x in idx[ptr[h]:ptr[h + 1]]] for h in range(len(ptr) - 1)}
+    hss = make_golden.DuckHss(d['coordinates'], d['radii'], copy_index, d['chrom'])
+    S = d['coordinates'].shape[1]
+    rng = np.random.RandomState(31)
+    two = np.array([h for h in range(len(ptr) - 1) if len(copy_index[h]) == 2])
+    loci = np.sort(rng.choice(two, 300, replace=False)).astype(np.int32)
+    pexp = rng.beta(2.0, 5.0, len(loci)).astype(np.float32)
+    pexp[:5] = 0.0
+    plast = np.where(rng.rand(len(loci)) < 0.5, rng.beta(2.0, 5.0, len(loci)), 0.0).astype(np.float32)
+    volumes_idx = [s % 2 for s in range(S)]
+    maps = [V.sphere_map(5500.0, 100.0, 3), V.sphere_map(5200.0, 100.0, 3)]
+    out = {'loci': loci, 'pexp': pexp, 'plast': plast, 'volumes_idx': np.array(volumes_idx, np.int32)}
+    with tempfile.TemporaryDirectory() as tmp:
+        prefix = os.path.join(tmp, 'nucleus_')
+        for m, vol in enumerate(maps):
+            V.write_volume(prefix + str(m) + '.bin', vol)
+            for key in ('nvoxel', 'center', 'origin', 'grid', 'matrice'):
+                out['m%d_%s' % (m, key)] = vol[key]
+        params = np.array([(i, p, q) for i, p, q in zip(loci, pexp, plast)], dtype=np.float32)
+        params = [(int(I), pe, pl) for I, pe, pl in params]
+        for it_corr in (0, 1):
+            rows = damid_mod.get_damid_actdist_exp(params, hss, S, copy_index, it_corr, contact_range=0.05,
+                                                   volumes_idx=volumes_idx, volume_prefix=prefix)
+            fmt = damid_mod.damid_actdist_fmt_str
+            name = os.path.join(tmp, 'rows.tmp')
+            with open(name, 'w') as f:
+                f.write('\n'.join([fmt % x for x in rows]))
+            rt = np.atleast_1d(np.genfromtxt(name, dtype=damid_mod.damid_actdist_shape))
+            out['c%d_loc' % it_corr] = rt['loc']
+            out['c%d_dist' % it_corr] = rt['dist']
+            out['c%d_prob' % it_corr] = rt['prob']
+    return out
 
 
 if __name__ == '__main__':

@@ -100,7 +100,7 @@ def test_damid_edges(pop):
     with pytest.raises(RuntimeError):
         damid.compute_damid_actdist(crd, radii, cp, ci, [len(cp) - 1], [0.5], [0.0], 1)
     with pytest.raises(NotImplementedError):
-        damid.compute_damid_actdist(crd, radii, cp, ci, [0], [0.5], [0.0], 1, shape='exp_map')
+        damid.compute_damid_actdist(crd, radii, cp, ci, [0], [0.5], [0.0], 1, shape='cylinder')
 
 
 def test_damid_per_locus_signature(pop):
@@ -270,3 +270,19 @@ def test_sprite_full_size_200kb(pop200):
         for s in range(0, 1000, 111):
             assert rg2[k, s] == rg[s], (c, s)
         assert np.array_equal(bi[k], A.keep_best(rg2[k], 50))
+
+
+@pytest.mark.parametrize('it_corr', [0, 1])
+def test_damid_exp_map_golden(pop, it_corr):
+    """exp_map DamID (get_damid_actdist_exp, py:475-577) on two maps assigned per
+    structure: rows bit-exact against the reference's."""
+    from igm_amd import damid
+    g = load_golden('damid_exp_golden.npz')
+    maps = [dict(body_idx=0, nvoxel=g['m%d_nvoxel' % m], center=g['m%d_center' % m], origin=g['m%d_origin' % m],
+                 grid=g['m%d_grid' % m], matrice=g['m%d_matrice' % m]) for m in (0, 1)]
+    rows = damid.compute_damid_actdist(pop['coordinates'], pop['radii'], pop['copy_ptr'], pop['copy_idx'], g['loci'],
+                                       g['pexp'], g['plast'], it_corr, 0.05, 'exp_map', volumes=maps,
+                                       struct_map=g['volumes_idx'])
+    assert np.array_equal(rows['loc'], g['c%d_loc' % it_corr])
+    assert np.array_equal(bits(rows['dist']), bits(g['c%d_dist' % it_corr]))
+    assert np.array_equal(bits(rows['prob']), bits(g['c%d_prob' % it_corr]))

@@ -89,3 +89,18 @@ def test_sprite_get_rgs2_known_answers():
                 v = A.rg2_f32([alts[i][comb[i]] for i in range(len(alts))])
                 best = min(best, v) if v < best else best
             assert best == g['kat%d_rg2s' % q][s]
+
+
+def exp_maps(g):
+    return [dict(body_idx=0, nvoxel=g['m%d_nvoxel' % m], center=g['m%d_center' % m], origin=g['m%d_origin' % m],
+                 grid=g['m%d_grid' % m], matrice=g['m%d_matrice' % m]) for m in (0, 1)]
+
+
+@pytest.mark.parametrize('it_corr', [0, 1])
+def test_damid_exp_oracle_equals_reference(pop, it_corr):
+    g = load_golden('damid_exp_golden.npz')
+    rows = A.damid_actdist_exp(pop['coordinates'], pop['copy_ptr'], pop['copy_idx'], g['loci'], g['pexp'],
+                               g['plast'], it_corr, 0.05, exp_maps(g), g['volumes_idx'])
+    assert np.array_equal(rows['loc'], g['c%d_loc' % it_corr])
+    assert np.array_equal(rows['dist'].view(np.uint32), g['c%d_dist' % it_corr].view(np.uint32))
+    assert np.array_equal(rows['prob'].view(np.uint32), g['c%d_prob' % it_corr].view(np.uint32))
