@@ -202,7 +202,7 @@ __host__ __device__ inline size_t carve_ws(void* base, int natom, int ldn, int k
     L->cell = cv.take<int>(cellcap + 8);
     L->nnb = cv.take<uint16_t>(ldn);
     L->sorted = cv.take<uint16_t>(ldn);
-    L->gell = cv.take<uint16_t>((size_t)ldn * kg);
+    L->gell = cv.take<uint16_t>((size_t)ldn * kg + 64 * IGM_PAIR_BATCH);  // slack for the batched reads
     L->kg = kg;
     L->lell = nullptr;
     L->lstride = 0;
@@ -466,17 +466,23 @@ __device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, ui
             const uint16_t* gl = L.gell + (size_t)(a >> 6) * L.kg * 64 + (a & 63);
             if constexpr (std::is_same<T, float>::value) {
                 // one batch of U neighbours of a slot sequence idx(k), k < n (tail masked)
+                // slots k0..k0+U-1 are always readable (LDS: kl is a multiple of U; HBM:
+                // the overflow regions carry U-1 slack slots); a slot past n holds a stale
+                // or scratch value, clamped to a valid atom and masked out.  Keeping the
+                // slot offset wave-uniform turns the address arithmetic scalar.
+                const int amax = P.natom - 1;
+                const float evfpi = evf * 0.318309886183790671537767526745f;
                 auto batch = [&](int k0, int n, auto idx) {
                     int jv[U];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) jv[u] = (int)idx(k0 + u < n ? k0 + u : n - 1);
+                    for (int u = 0; u < U; ++u) jv[u] = min((int)idx(k0 + u), amax);
                     float4 pj[U];
 #pragma unroll
                     for (int u = 0; u < U; ++u) pj[u] = pos[jv[u]];
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const float dx = xi - pj[u].x, dy = yi - pj[u].y, dz = zi - pj[u].z;
-                        const float fp = soft_pair_bf(dx * dx + dy * dy + dz * dz, ri + pj[u].w, evf);
+                        const float fp = soft_pair_bf(dx * dx + dy * dy + dz * dz, ri + pj[u].w, evfpi);
                         const float m = (k0 + u < n) ? fp : 0.0f;
                         fx += m * dx;
                         fy += m * dy;
@@ -484,7 +490,7 @@ __device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, ui
                     }
                 };
                 const uint16_t* ll = L.lell + a;
-                const int ls = L.lstride;
+                const int ls = __builtin_amdgcn_readfirstlane(L.lstride);  // uniform: scalar slot offsets
                 for (int k0 = 0; k0 < n1; k0 += U) batch(k0, n1, [&](int k) { return ll[(size_t)k * ls]; });
                 const int n2 = nn - n1;
                 for (int k0 = 0; k0 < n2; k0 += U) batch(k0, n2, [&](int k) { return gl[(size_t)k * 64]; });
@@ -2350,7 +2356,9 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
         IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int grid = 0;
         IGM_TRY(resident_grid(c, kern, NT, lds, pr.cm.nstruct, &grid));
-        A.ws_stride = ((size_t)pr.cm.ldn * (pr.cm.kcap - kLdsListSlots) * 2 + 255) & ~size_t(255);
+        // + slack: the batched force loop reads up to IGM_PAIR_BATCH - 1 slots past a list
+        A.ws_stride = ((size_t)pr.cm.ldn * (pr.cm.kcap - kLdsListSlots) * 2 + 64 * 2 * IGM_PAIR_BATCH + 255) &
+                      ~size_t(255);
         void* ws;
         IGM_TRY(workspace(c, "ms_ldsovf", A.ws_stride * (size_t)grid, &ws));
         A.ws = (unsigned char*)ws;

@@ -175,13 +175,14 @@ __device__ __forceinline__ T bond_term(T r2, T r0, T k, bool lower, double& e) {
 }
 
 // branch-free f32 soft pair (the MD kernels): f/r multiplier, 0 outside the cutoff
-// or for coincident atoms; all candidates of a batch evaluate together
-__device__ __forceinline__ float soft_pair_bf(float r2, float rc, float evf) {
-    const float inv_pi = 0.318309886183790671537767526745f;
-    const float rinv = __frsqrt_rn(fmaxf(r2, 1.0e-30f));
+// or for coincident atoms; all candidates of a batch evaluate together.  evfpi =
+// evf / pi; the hardware v_rsq / v_rcp (1 ulp) stand in for the correctly rounded
+// forms, whose denormal-safe expansions cost 5 VALU ops each on gfx950.
+__device__ __forceinline__ float soft_pair_bf(float r2, float rc, float evfpi) {
+    const float rinv = __builtin_amdgcn_rsqf(fmaxf(r2, 1.0e-30f));
     const float r = r2 * rinv;
-    const float s = __builtin_amdgcn_sinf(0.5f * r * __frcp_rn(rc));  // sin(pi r / rc): v_sin takes revolutions
-    const float f = evf * rc * inv_pi * s * rinv;
+    const float s = __builtin_amdgcn_sinf(r * (0.5f * __builtin_amdgcn_rcpf(rc)));  // sin(pi r / rc), in revolutions
+    const float f = (evfpi * rc) * s * rinv;
     return (r2 < rc * rc && r2 > 0.0f) ? f : 0.0f;
 }
 
