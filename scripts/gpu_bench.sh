@@ -1,5 +1,7 @@
 #!/bin/bash
 # Full bench line + rocprofv3 kernel trace + PMC HBM-traffic passes (one pass per run).
+# The profiled runs use the bench's own step/warmup counts, so the per-launch anneal
+# durations in the trace line up with the bench's timed launches (warmup = launch 1).
 # usage: bash scripts/gpu_bench.sh <tag>   -> gpurun_out/<tag>/...
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-r01}
@@ -10,7 +12,7 @@ export TMPDIR=/tmp
 BARGS=${BARGS:-}
 timeout -k 10 900 python -u bench.py $BARGS > $OUT/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
-PARGS="--steps 1 --warmup 0 --cpu-sample 0 $BARGS"
+PARGS="--steps 2 --warmup 1 --cpu-sample 0 --no-de $BARGS"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt -- python3 bench.py $PARGS > $OUT/prof_kt.log 2>&1
 rc=$?; echo "kt rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch -- python3 bench.py $PARGS > $OUT/prof_fetch.log 2>&1
