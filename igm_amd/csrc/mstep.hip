@@ -2130,6 +2130,13 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
     out->cm.kcap = kcap;
     LaunchCfg cfg;
     out->big = (prm->flags & IGM_MSTEP_FORCE_GLOBAL) || getenv("IGM_FORCE_POP") || !lds_fits(natom, &cfg);
+    if (out->big && !(prm->skin > 0) && !getenv("IGM_SKIN_FACTOR")) {
+        // the HBM engine gathers neighbours from L2/MALL: a tighter list (skin 0.55
+        // maxrad, scripts/gpu_skin.sh on config C) beats the extra rebuilds
+        const float rmax = 0.5f * (P.cut_list - P.skin);
+        P.skin = 0.55f * rmax;
+        P.cut_list = 2.0f * rmax + P.skin;
+    }
     out->P = P;
     return IGM_OK;
 }
