@@ -216,7 +216,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     de = None
-    if rank == 0 and not args.no_de:
+    if rank == 0 and world == 1 and not args.no_de:  # the N=1 line carries it; scaling runs stay lean
         de = bench_asteps_de(args, it.ctx)
     score = it.violation_score()
     info = it.info_host()

@@ -78,3 +78,55 @@ def test_two_rank_astep_rows_equal_single_rank(tmp_path):
                             pop['copy_idx'], pop['chrom'], pairs, 2.0, 1)
     assert got.tobytes() == ref.tobytes()
     assert len(ref) > 500
+
+
+def _de_worker(rank, world, port, out):
+    """Configuration D/E A-steps over the gathered population: DamID loci and FISH
+    probes sharded in contiguous ranges, results gathered in rank order (the oracle
+    standing in for the HIP kernels, which the gpu tests pin to the same oracle)."""
+    from oracle import asteps as A
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        pop, _, xyz_sm = _inputs()
+        S = xyz_sm.shape[0]
+        s0, s1 = pipeline.shard(S, rank, world)
+        full = pipeline.gather_population(torch.from_numpy(xyz_sm[s0:s1].copy())).numpy()
+        bm = np.ascontiguousarray(full.transpose(1, 0, 2))
+        nhap = len(pop['copy_ptr']) - 1
+        prof = np.random.default_rng(1).beta(2.0, 5.0, nhap).astype(np.float32)
+        loci = np.where(prof >= 0.3)[0].astype(np.int32)
+        lo, hi = pipeline.shard(len(loci), rank, world)
+        rows = A.damid_actdist(bm, pop['radii'], pop['copy_ptr'], pop['copy_idx'], loci[lo:hi], prof,
+                               np.zeros(nhap, np.float32), 1, 0.05, 'sphere', 5500.0)
+        allrows, n = pipeline.gather_rows(torch.from_numpy(rows.view(np.uint8).copy()), len(rows), 12)
+        probes = loci[:40]
+        t = np.sort(np.random.default_rng(2).lognormal(7.5, 0.4, (len(probes), S)), axis=1).astype(np.float32)
+        plo, phi = pipeline.shard(len(probes), rank, world)
+        omin, _, _, _ = A.fish_radial(bm, pop['copy_ptr'], pop['copy_idx'], probes[plo:phi], t[plo:phi], t[plo:phi])
+        allf, nf = pipeline.gather_rows(torch.from_numpy(omin.view(np.uint8).ravel().copy()), len(omin), 4 * S)
+        if rank == 0:
+            np.savez(out, damid=allrows.numpy(), fish=allf.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_de_asteps_equal_single_rank(tmp_path):
+    from oracle import asteps as A
+    out = str(tmp_path / 'de.npz')
+    mp.spawn(_de_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    pop, _, xyz_sm = _inputs()
+    bm = np.ascontiguousarray(xyz_sm.transpose(1, 0, 2))
+    S = xyz_sm.shape[0]
+    nhap = len(pop['copy_ptr']) - 1
+    prof = np.random.default_rng(1).beta(2.0, 5.0, nhap).astype(np.float32)
+    loci = np.where(prof >= 0.3)[0].astype(np.int32)
+    ref = A.damid_actdist(bm, pop['radii'], pop['copy_ptr'], pop['copy_idx'], loci, prof, np.zeros(nhap, np.float32),
+                          1, 0.05, 'sphere', 5500.0)
+    assert got['damid'].tobytes() == ref.tobytes() and len(ref) > 100
+    probes = loci[:40]
+    t = np.sort(np.random.default_rng(2).lognormal(7.5, 0.4, (len(probes), S)), axis=1).astype(np.float32)
+    omin, _, _, _ = A.fish_radial(bm, pop['copy_ptr'], pop['copy_idx'], probes, t, t)
+    assert got['fish'].tobytes() == omin.tobytes()
