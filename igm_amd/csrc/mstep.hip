@@ -49,6 +49,7 @@ constexpr int kLdsListSlots = 8;          // LDS path: the first slots of every 
 #ifndef IGM_PAIR_BATCH
 #define IGM_PAIR_BATCH 4
 #endif
+constexpr int kPopPairBatch = 8;  // HBM engine: neighbours per batch (more loads in flight, VGPRs allow it)
 
 // ------------------------------------------------------------------ carving
 struct Carver {
@@ -202,7 +203,7 @@ __host__ __device__ inline size_t carve_ws(void* base, int natom, int ldn, int k
     L->cell = cv.take<int>(cellcap + 8);
     L->nnb = cv.take<uint16_t>(ldn);
     L->sorted = cv.take<uint16_t>(ldn);
-    L->gell = cv.take<uint16_t>((size_t)ldn * kg + 64 * IGM_PAIR_BATCH);  // slack for the batched reads
+    L->gell = cv.take<uint16_t>((size_t)ldn * kg + 64 * kPopPairBatch);  // slack for the batched reads
     L->kg = kg;
     L->lell = nullptr;
     L->lstride = 0;
@@ -447,7 +448,7 @@ __device__ __noinline__ void pair_walk(int a, T xi, T yi, T zi, T ri, const vec4
 
 // Total force on atom a, gathered by its owner thread: pairs from the Verlet
 // list (or the cell walk around the build-time position b*), bonds B, envelopes.
-template <typename T, bool EN, typename OffT>
+template <typename T, bool EN, typename OffT, int PB = IGM_PAIR_BATCH>
 __device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, uint32_t fl, const vec4_t<T>* pos,
                                            const NList<T, OffT>& L, T bx, T by, T bz, const BondView& B,
                                            const DevParams& P, T evf, T envf, T& fx, T& fy,
@@ -461,7 +462,7 @@ __device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, ui
             pair_walk<T, EN, OffT>(a, xi, yi, zi, ri, pos, L, bx, by, bz, P, evf, fx, fy, fz, ep);
         } else if (nn > 0) {
             // the LDS slots, then the HBM slots, in batches whose loads are all in flight together
-            constexpr int U = IGM_PAIR_BATCH;
+            constexpr int U = PB;  // neighbours whose loads are in flight together
             const int n1 = nn < L.kl ? nn : L.kl;
             const uint16_t* gl = L.gell + (size_t)(a >> 6) * L.kg * 64 + (a & 63);
             if constexpr (std::is_same<T, float>::value) {
@@ -1151,7 +1152,7 @@ __global__ void __launch_bounds__(kPopBS) pop_forces_kernel(PopArgs A, float evf
     const float4 b = A.xb4[i];
     double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
     float fx, fy, fz;
-    atom_force<float, false, int>(s, a, W.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], W.pos, L, b.x, b.y, b.z, B, A.P, evf, envf, fx, fy,
+    atom_force<float, false, int, kPopPairBatch>(s, a, W.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], W.pos, L, b.x, b.y, b.z, B, A.P, evf, envf, fx, fy,
                                   fz, ep, eb, ee);
     A.f4[i] = make_float4(fx, fy, fz, 0.f);
 }
