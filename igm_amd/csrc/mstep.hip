@@ -46,10 +46,20 @@ constexpr int kCellCapBig = 32768;        // cell grid of an HBM-resident struct
 constexpr size_t kLdsBytes = 160 * 1024 - 1024;  // dynamic LDS per workgroup: 160 KB per CU (gfx950) less a static reserve
 constexpr int kNeighBudget = 64;          // default Verlet-list slots per atom
 constexpr int kLdsListSlots = 8;          // LDS path: the first slots of every atom's list live in LDS
+#ifndef IGM_BOND_BATCH
+#define IGM_BOND_BATCH 2  // LDS bonds per batch (config B anneal: 2 is 1.1% faster than 4)
+#endif
 #ifndef IGM_PAIR_BATCH
 #define IGM_PAIR_BATCH 4
 #endif
 constexpr int kPopPairBatch = 8;  // HBM engine: neighbours per batch (more loads in flight, VGPRs allow it)
+// LDS anneal kernel: neighbours per batch.  LDS latency is short and lists are short, so
+// the masked tail of a wide batch costs more than the extra loads in flight win
+// (measured config B, anneal: batch 2 1700 ms, 1 1761 ms, 4 1779 ms, 8 1907 ms)
+#ifndef IGM_LDS_PAIR_BATCH
+#define IGM_LDS_PAIR_BATCH 2
+#endif
+constexpr int kLdsPairBatch = IGM_LDS_PAIR_BATCH;
 
 // ------------------------------------------------------------------ carving
 struct Carver {
@@ -272,9 +282,12 @@ __device__ __forceinline__ int cell_index(T x, T y, T z, const T* lo, const T* i
 }
 
 // visit the beads of the 27 cells around cell c (x-runs are contiguous in `sorted`):
-// f(j, valid) in batches of 4 -- the bead ids of a batch are loaded together so the
+// f(j, valid) in batches of WB -- the bead ids of a batch are loaded together so the
 // dependent LDS reads overlap; an invalid slot carries a valid id (masked by caller)
-template <typename OffT, typename F>
+#ifndef IGM_WALK_BATCH
+#define IGM_WALK_BATCH 4
+#endif
+template <int WB = IGM_WALK_BATCH, typename OffT, typename F>
 __device__ __forceinline__ void walk27(int c, const OffT* cell, const uint16_t* sorted, const int* gn, F&& f) {
     const int nx = gn[0], ny = gn[1], nz = gn[2];
     const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
@@ -287,12 +300,12 @@ __device__ __forceinline__ void walk27(int c, const OffT* cell, const uint16_t* 
             const int row = (z0 * ny + y0) * nx;
             const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
             const int beg = (int)cell[row + xlo], end = (int)cell[row + xhi + 1];
-            for (int q = beg; q < end; q += 4) {
-                int jj[4];
+            for (int q = beg; q < end; q += WB) {
+                int jj[WB];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) jj[u] = (int)sorted[q + u < end ? q + u : beg];
+                for (int u = 0; u < WB; ++u) jj[u] = (int)sorted[q + u < end ? q + u : beg];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) f(jj[u], q + u < end);
+                for (int u = 0; u < WB; ++u) f(jj[u], q + u < end);
             }
         }
     }
@@ -511,7 +524,7 @@ __device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, ui
         }
     }
     if (B.l && B.n > 0) {
-        constexpr int UL = 4;  // LDS bond entries per batch, branch-free
+        constexpr int UL = IGM_BOND_BATCH;  // LDS bond entries per batch, branch-free
         for (int k0 = 0; k0 < B.n; k0 += UL) {
             uint32_t ev[UL];
 #pragma unroll
@@ -785,7 +798,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                         const BondView B = lds_bonds ? BondView{nullptr, nullptr, sm.rest + sm.boff[a], sm.btab,
                                                                 (int)sm.boff[a + 1] - (int)sm.boff[a]}
                                                      : BondView{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
-                        atom_force<float, false, uint16_t>(s, a, sm.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], sm.pos, sm.L,
+                        atom_force<float, false, uint16_t, kLdsPairBatch>(s, a, sm.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], sm.pos, sm.L,
                                                            pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
                                                            pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz, ep,
                                                            eb, ee);
