@@ -106,7 +106,8 @@ def bench_asteps_de(args, ctx):
     """Configuration D/E A-steps at full population size (200 kb diploid, 1000
     structures, bead-major .hss layout resident in HBM), timed with HIP events around
     each kernel family: DamID (ellipsoid, sigma 0.45), FISH (500 probes + 500 pairs),
-    SPRITE (Rg^2 of every (cluster, structure) + keep_best 50).  Outside the timed
+    SPRITE (Rg^2 of every (cluster, structure) + keep_best 50), polymer distances
+    (every (i, i+1) locus, PolymerAssignmentStep).  Outside the timed
     A/M region; reported beside it.  Algorithmic bytes: the unique coordinate columns
     each unit reads (12 B per bead per structure) plus its inputs/outputs."""
     import torch
@@ -147,6 +148,18 @@ def bench_asteps_de(args, ctx):
               (4 + 4) * 50 * len(t['kept']) + 4 * 50 * len(t['seg_region']))
     out['sprite'] = {'units': int(len(t['kept'])), 'unit': 'clusters x 1000 structures', 'ms': ms,
                      'algorithmic_bytes': b, 'achieved_GBps': b / (ms * 1e-3) / 1e9}
+    # polymer distances: every (i, i+1) locus, 60-bin distribution, one launch
+    from igm_amd import polymer
+    nb = xyz.shape[0]
+    edges = np.linspace(200.0, 900.0, 60)
+    prob = np.exp(-0.5 * ((edges - 500.0) / 120.0) ** 2)
+    prob /= prob.sum()
+    for _ in range(2):
+        polymer.assign(xyz, edges, prob, np.random.RandomState(1), chunk=nb, ctx=ctx)
+    ms = ctx.kernel_ms('polymer')
+    b = float((nb - 1) * S * (24.0 + 8.0 + 4.0))
+    out['polymer'] = {'units': int(nb - 1), 'unit': 'loci x 1000 structures', 'ms': ms, 'algorithmic_bytes': b,
+                      'achieved_GBps': b / (ms * 1e-3) / 1e9}
     out['workload'] = '200 kb diploid (29 838 beads), 1000 structures, bead-major f32 in HBM'
     del torch
     return out

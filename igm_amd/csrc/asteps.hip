@@ -17,6 +17,9 @@
 // bit-identical to the reference's.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <vector>
+
 #include <hipcub/hipcub.hpp>
 
 #include "exact_math.h"
@@ -591,6 +594,98 @@ __global__ void __launch_bounds__(kBT) sprite_keep_best_kernel(const float* __re
     }
 }
 
+// ============================================================================ polymer
+// PolymerAssignmentStep.task (igm/steps/PolymerAssignmentStep.py:84-129): for locus i,
+// the S distances |x_i - x_(i+1)| (get_polymer_dists, :24-32, float32 norms) are
+// ranked -- argsort(argsort(d)), ties in structure order -- and structure s receives
+// the rank-th smallest of S distances drawn from the bin distribution
+// (np.sort(np.random.choice(edges, S, p=prob)), :113).  The draws arrive as the
+// uniforms random_sample() produced for that choice; the bin of a draw is
+// cdf.searchsorted(u, side='right') as RandomState.choice computes it.  The sorted
+// draws are never materialised: a per-locus histogram over the bins in VALUE order,
+// prefix-summed, answers "rank-th smallest" by binary search.
+struct PolymerArgs {
+    const float* xyz;    // (nbead, S, 3)
+    int S;
+    const int* loci;
+    int nloci;
+    const double* u;     // (nloci, S)
+    int nbins;
+    const double* cdf;   // (nbins) p.cumsum() / last
+    const int* vpos;     // (nbins) position of each bin in value order
+    const double* vsort; // (nbins) bin values in value order
+    float* out;          // (nloci, S)
+    float* dist;         // (nloci, S) or null
+};
+
+__global__ void __launch_bounds__(kBT) polymer_kernel(PolymerArgs A) {
+    extern __shared__ float psm[];
+    const int q = blockIdx.x;
+    if (q >= A.nloci) return;
+    const int S = A.S, nb = A.nbins, t = threadIdx.x;
+    float* d = psm;
+    int* cnt = reinterpret_cast<int*>(psm + S);  // nb counts, then the inclusive prefix
+    for (int b = t; b < nb; b += kBT) cnt[b] = 0;
+    __syncthreads();
+    const int i = A.loci[q];
+    const double* u = A.u + (size_t)q * S;
+    for (int s = t; s < S; s += kBT) {
+        float x, y, z, a, b, c;
+        load3(A.xyz, S, i, s, x, y, z);
+        load3(A.xyz, S, i + 1, s, a, b, c);
+        d[s] = norm3(__fsub_rn(x, a), __fsub_rn(y, b), __fsub_rn(z, c));
+        const double uv = u[s];
+        int lo = 0, hi = nb;  // first k with cdf[k] > u
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (A.cdf[mid] <= uv) lo = mid + 1;
+            else hi = mid;
+        }
+        atomicAdd(&cnt[A.vpos[lo < nb ? lo : nb - 1]], 1);
+    }
+    __syncthreads();
+    if (t < 64) {  // inclusive prefix over the bins: one wave, a chunk per lane
+        const int per = (nb + 63) / 64, b0 = t * per, b1 = min(nb, b0 + per);
+        int run = 0;
+        for (int b = b0; b < b1; ++b) run += cnt[b];
+        int incl = run;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (t >= o) incl += v;
+        }
+        run = incl - run;
+        for (int b = b0; b < b1; ++b) {
+            run += cnt[b];
+            cnt[b] = run;
+        }
+    }
+    __syncthreads();
+    const size_t row = (size_t)q * S;
+    for (int s = t; s < S; s += kBT) {
+        const float ds = d[s];
+        int r = 0, k = 0;
+        for (; k + 4 <= S; k += 4) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const float e = d[k + w];
+                r += (e < ds) | ((e == ds) & (k + w < s));
+            }
+        }
+        for (; k < S; ++k) {
+            const float e = d[k];
+            r += (e < ds) | ((e == ds) & (k < s));
+        }
+        int lo = 0, hi = nb - 1;  // first value position whose prefix count exceeds r
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cnt[mid] > r) hi = mid;
+            else lo = mid + 1;
+        }
+        A.out[row + s] = __double2float_rn(A.vsort[lo]);
+        if (A.dist) A.dist[row + s] = ds;
+    }
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -894,5 +989,65 @@ extern "C" int igm_sprite_assign(igm_ctx* c, uint32_t flags, const float* xyz, i
         IGM_TRY(to_host(c, flags, best_rg2, d_bv, nb));
         IGM_TRY(to_host(c, flags, best_sel, d_bs, nbs));
     }
+    return finish(c, flags);
+}
+
+extern "C" int igm_polymer_assign(igm_ctx* c, uint32_t flags, const float* xyz, int32_t nbead, int32_t nstruct,
+                                  const int32_t* loci, int32_t nloci, const double* uniforms, int32_t nbins,
+                                  const double* edges, const double* prob, float* nn_dist, float* dist) {
+    if (!c) return IGM_E_INVALID;
+    if (nbead < 2 || nstruct <= 0 || nloci < 0 || nbins <= 0 || !xyz || !edges || !prob ||
+        (nloci > 0 && (!loci || !uniforms || !nn_dist)))
+        return fail(c, IGM_E_INVALID, "igm_polymer_assign: invalid arguments");
+    const size_t lds = (size_t)nstruct * sizeof(float) + (size_t)nbins * sizeof(int);
+    if (lds > (size_t)160 * 1024 - 1024)
+        return fail(c, IGM_E_UNSUPPORTED, "igm_polymer_assign: %d structures x %d bins exceed the LDS-resident kernel",
+                    nstruct, nbins);
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    if (nloci == 0) return IGM_OK;
+    if (flags & IGM_DEVICE_PTRS)
+        return fail(c, IGM_E_UNSUPPORTED, "igm_polymer_assign: host distribution arrays expected");
+    for (int32_t k = 0; k < nloci; ++k)
+        if (loci[k] < 0 || loci[k] >= nbead - 1)
+            return fail(c, IGM_E_INVALID, "igm_polymer_assign: locus %d outside [0, %d)", loci[k], nbead - 1);
+    // RandomState.choice: cdf = p.cumsum(); cdf /= cdf[-1] (sequential float64 sums)
+    std::vector<double> cdf(nbins);
+    double run = 0.0;
+    for (int b = 0; b < nbins; ++b) cdf[b] = run += prob[b];
+    const double last = cdf[nbins - 1];
+    for (int b = 0; b < nbins; ++b) cdf[b] /= last;
+    // the bins in value order (np.sort of the drawn values)
+    std::vector<int> order(nbins), vpos(nbins);
+    for (int b = 0; b < nbins; ++b) order[b] = b;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return edges[x] < edges[y]; });
+    std::vector<double> vsort(nbins);
+    for (int k = 0; k < nbins; ++k) {
+        vpos[order[k]] = k;
+        vsort[k] = edges[order[k]];
+    }
+    const size_t nout = (size_t)nloci * nstruct;
+    const float* d_xyz;
+    const int32_t *d_loci, *d_vpos;
+    const double *d_u, *d_cdf, *d_vsort;
+    IGM_TRY(to_device(c, flags, "po_xyz", xyz, (size_t)nbead * nstruct * 3, &d_xyz));
+    IGM_TRY(to_device(c, flags, "po_loci", loci, (size_t)nloci, &d_loci));
+    IGM_TRY(to_device(c, flags, "po_u", uniforms, nout, &d_u));
+    IGM_TRY(to_device(c, flags, "po_cdf", (const double*)cdf.data(), (size_t)nbins, &d_cdf));
+    IGM_TRY(to_device(c, flags, "po_vpos", (const int32_t*)vpos.data(), (size_t)nbins, &d_vpos));
+    IGM_TRY(to_device(c, flags, "po_vsort", (const double*)vsort.data(), (size_t)nbins, &d_vsort));
+    float *d_out, *d_dist;
+    IGM_TRY(out_device(c, flags, "po_out", nn_dist, nout, &d_out));
+    IGM_TRY(out_device(c, flags, "po_dist", dist, nout, &d_dist));
+    if (lds > 65536)
+        IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)polymer_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds));
+    PolymerArgs A{d_xyz, nstruct, d_loci, nloci, d_u, nbins, d_cdf, d_vpos, d_vsort, d_out, d_dist};
+    {
+        Timed tm(c, "polymer");
+        hipLaunchKernelGGL(polymer_kernel, dim3((unsigned)nloci), dim3(kBT), lds, c->stream, A);
+        IGM_HIP_CHECK(c, hipGetLastError());
+    }
+    IGM_TRY(to_host(c, flags, nn_dist, d_out, nout));
+    IGM_TRY(to_host(c, flags, dist, d_dist, nout));
     return finish(c, flags);
 }

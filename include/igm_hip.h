@@ -149,6 +149,22 @@ int igm_fish_assign(igm_ctx* ctx, uint32_t flags,
                     const float* target_min, const float* target_max,
                     float* out_min, float* out_max, float* dist_min, float* dist_max);
 
+/* Polymer distances: PolymerAssignmentStep.task (igm/steps/PolymerAssignmentStep.py:
+ * 84-129) for all loci at once.  For locus i (0 <= i < nbead - 1) the S float32
+ * distances |x_i - x_(i+1)| (get_polymer_dists, :24-32) are ranked -- argsort(argsort)
+ * with ties in structure order -- and structure s receives the rank-th smallest of the
+ * S values drawn by np.random.choice(edges, S, p=prob) (:113): uniforms[q, s] are the
+ * random_sample() draws of that call for loci[q] (the caller's RandomState, in the
+ * reference's locus order), a draw's bin is searchsorted(cumsum(p) / sum, u, 'right').
+ * nn_dist (nloci, nstruct) f32 = the float64 edge value rounded to float32 (the 'f4'
+ * dataset of reduce(), :158-162); dist (nloci, nstruct) f32 or NULL.  Host pointers
+ * for edges / prob (nbins float64 each). */
+int igm_polymer_assign(igm_ctx* ctx, uint32_t flags,
+                       const float* xyz, int32_t nbead, int32_t nstruct,
+                       const int32_t* loci, int32_t nloci, const double* uniforms,
+                       int32_t nbins, const double* edges, const double* prob,
+                       float* nn_dist, float* dist);
+
 /* SPRITE: SpriteAssignmentStep.task (igm/steps/SpriteAssignmentStep.py:105-160):
  * compute_gyration_radius (igm/cython_compiled/sprite.pyx:104-283, get_rg2s_cpp
  * cpp_sprite_assignment.cpp:49-143) for every (cluster, structure), then keep_best.

@@ -9,6 +9,8 @@ tests/golden/make_golden_asteps.py produced by running the reference itself.
   sprite_cluster_rg2     cython_compiled/sprite.pyx:104-283 with get_rg2s_cpp
                          (cpp_sprite_assignment.cpp:49-143)
   keep_best              steps/SpriteAssignmentStep.py:138-143
+  polymer_assign         steps/PolymerAssignmentStep.py:24-32,84-129 (golden vectors:
+                         tests/golden/make_golden_polymer.py, the reference run here)
 """
 import numpy as np
 
@@ -231,4 +233,20 @@ def damid_actdist_exp(crd, copy_ptr, copy_idx, loci, pexp, plast, it_corr, conta
     out = np.zeros(len(rows), [('loc', 'i4'), ('dist', 'f4'), ('prob', 'f4')])
     if rows:
         out['loc'], out['dist'], out['prob'] = zip(*rows)
+    return out
+
+
+def polymer_assign(crd, loci, edges, prob, rng):
+    """PolymerAssignmentStep.task for `loci` in order, drawing from `rng` (a RandomState)
+    as the reference draws from np.random: per locus np.sort(choice(edges, S, p)), the
+    float32 norms |x_i - x_(i+1)| ranked (argsort(argsort), ties in structure order --
+    the reference's default quicksort leaves exact ties unspecified) and the sorted
+    draws indexed by rank; returned as the reduce() 'f4' dataset."""
+    S = crd.shape[1]
+    out = np.zeros((len(loci), S), np.float32)
+    for q, i in enumerate(loci):
+        sampled = np.sort(rng.choice(edges, S, p=prob))
+        d = np.linalg.norm(crd[i, :, :] - crd[i + 1, :, :], axis=1)
+        idx = np.argsort(np.argsort(d, kind='stable'), kind='stable')
+        out[q] = sampled[idx]
     return out
