@@ -1051,3 +1051,109 @@ extern "C" int igm_polymer_assign(igm_ctx* c, uint32_t flags, const float* xyz, 
     IGM_TRY(to_host(c, flags, dist, d_dist, nout));
     return finish(c, flags);
 }
+
+// ============================================================================ contact map
+// HicEvaluationStep.reduce (igm/steps/HicEvaluationStep.py:96-179) builds the simulated
+// Hi-C map of the population with alabtools' HssFile.buildContactMap(contactRange) (:109)
+// before summing the copies.  counts[i, j] = the number of structures with
+// |x_i - x_j| <= fl32(contact_range * fl32(r_i + r_j)), the float32 norm of the A/M
+// contact test (inter_hic.py:47) against the Hi-C restraint's r0 (hic.py).  One
+// workgroup per 64x64 bead tile (upper triangle, mirrored on store); the structures
+// stream through LDS in chunks of kCS, each thread keeps a 4x4 block of counters.
+namespace {
+constexpr int kCT = 64;  // beads per tile side
+constexpr int kCS = 32;  // structures per LDS chunk
+constexpr int kCRow = kCS * 3 + 1;  // padded LDS row (floats)
+
+__global__ void __launch_bounds__(kBT) contact_map_kernel(const float* __restrict__ xyz, int n, int S,
+                                                          const float* __restrict__ radii, float cr,
+                                                          int* __restrict__ counts) {
+    const int bi = blockIdx.y, bj = blockIdx.x;
+    if (bj < bi) return;  // upper-triangle tiles only (whole workgroup exits together)
+    __shared__ float li[kCT * kCRow];
+    __shared__ float lj[kCT * kCRow];
+    const int t = threadIdx.x, ti = t >> 4, tj = t & 15;
+    const int i0 = bi * kCT, j0 = bj * kCT;
+    float thr[4][4];
+    int cnt[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int i = min(i0 + ti * 4 + a, n - 1);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int j = min(j0 + tj * 4 + b, n - 1);
+            thr[a][b] = __fmul_rn(cr, __fadd_rn(radii[i], radii[j]));
+            cnt[a][b] = 0;
+        }
+    }
+    for (int s0 = 0; s0 < S; s0 += kCS) {
+        const int ns = min(kCS, S - s0), w = ns * 3;
+        __syncthreads();
+        for (int e = t; e < kCT * kCS * 3; e += kBT) {  // stage both bead blocks' chunk rows
+            const int r = e / (kCS * 3), c = e - r * (kCS * 3);
+            float vi = 0.f, vj = 0.f;
+            if (c < w) {
+                if (i0 + r < n) vi = xyz[((size_t)(i0 + r) * S + s0) * 3 + c];
+                if (j0 + r < n) vj = xyz[((size_t)(j0 + r) * S + s0) * 3 + c];
+            }
+            li[r * kCRow + c] = vi;
+            lj[r * kCRow + c] = vj;
+        }
+        __syncthreads();
+        for (int s = 0; s < ns; ++s) {
+            float xi[4][3], xj[4][3];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    xi[a][k] = li[(ti * 4 + a) * kCRow + s * 3 + k];
+                    xj[a][k] = lj[(tj * 4 + a) * kCRow + s * 3 + k];
+                }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const float d = norm3(__fsub_rn(xi[a][0], xj[b][0]), __fsub_rn(xi[a][1], xj[b][1]),
+                                          __fsub_rn(xi[a][2], xj[b][2]));
+                    cnt[a][b] += d <= thr[a][b];
+                }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int i = i0 + ti * 4 + a;
+        if (i >= n) continue;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int j = j0 + tj * 4 + b;
+            if (j >= n) continue;
+            counts[(size_t)i * n + j] = cnt[a][b];
+            counts[(size_t)j * n + i] = cnt[a][b];
+        }
+    }
+}
+}  // namespace
+
+extern "C" int igm_contact_map(igm_ctx* c, uint32_t flags, const float* xyz, int32_t nbead, int32_t nstruct,
+                               const float* radii, double contact_range, int32_t* counts) {
+    if (!c) return IGM_E_INVALID;
+    if (nbead <= 0 || nstruct <= 0 || !xyz || !radii || !counts || !(contact_range >= 0.0))
+        return fail(c, IGM_E_INVALID, "igm_contact_map: invalid arguments");
+    const int nt = (int)ceil_div(nbead, kCT);
+    if (nt > 65535) return fail(c, IGM_E_UNSUPPORTED, "igm_contact_map: %d beads exceed the tile grid", nbead);
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    const float* d_xyz;
+    const float* d_radii;
+    IGM_TRY(to_device(c, flags, "cm_xyz", xyz, (size_t)nbead * nstruct * 3, &d_xyz));
+    IGM_TRY(to_device(c, flags, "cm_radii", radii, (size_t)nbead, &d_radii));
+    int32_t* d_cnt;
+    IGM_TRY(out_device(c, flags, "cm_counts", counts, (size_t)nbead * nbead, &d_cnt));
+    {
+        Timed tm(c, "contact_map");
+        hipLaunchKernelGGL(contact_map_kernel, dim3((unsigned)nt, (unsigned)nt), dim3(kBT), 0, c->stream, d_xyz,
+                           (int)nbead, (int)nstruct, d_radii, (float)contact_range, (int*)d_cnt);
+        IGM_HIP_CHECK(c, hipGetLastError());
+    }
+    IGM_TRY(to_host(c, flags, counts, d_cnt, (size_t)nbead * nbead));
+    return finish(c, flags);
+}

@@ -165,6 +165,17 @@ int igm_polymer_assign(igm_ctx* ctx, uint32_t flags,
                        int32_t nbins, const double* edges, const double* prob,
                        float* nn_dist, float* dist);
 
+/* Population contact map: the simulated Hi-C counts HicEvaluationStep.reduce
+ * (igm/steps/HicEvaluationStep.py:96-179) builds with HssFile.buildContactMap
+ * (contactRange) at :109 (alabtools, absent here: the contact test restated is the
+ * IGM Hi-C one, |x_i - x_j| (float32 norm, inter_hic.py:47) <= fl32(contact_range *
+ * fl32(r_i + r_j))).  counts (nbead, nbead) int32, symmetric, diagonal included, =
+ * the number of structures in contact; the caller divides by nstruct and sums the
+ * copies (Contactmatrix.sumCopies, :111-112). */
+int igm_contact_map(igm_ctx* ctx, uint32_t flags,
+                    const float* xyz, int32_t nbead, int32_t nstruct,
+                    const float* radii, double contact_range, int32_t* counts);
+
 /* SPRITE: SpriteAssignmentStep.task (igm/steps/SpriteAssignmentStep.py:105-160):
  * compute_gyration_radius (igm/cython_compiled/sprite.pyx:104-283, get_rg2s_cpp
  * cpp_sprite_assignment.cpp:49-143) for every (cluster, structure), then keep_best.

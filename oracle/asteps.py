@@ -9,6 +9,7 @@ tests/golden/make_golden_asteps.py produced by running the reference itself.
   sprite_cluster_rg2     cython_compiled/sprite.pyx:104-283 with get_rg2s_cpp
                          (cpp_sprite_assignment.cpp:49-143)
   keep_best              steps/SpriteAssignmentStep.py:138-143
+  contact_counts         steps/HicEvaluationStep.py:109 (buildContactMap; parity unpinned)
   polymer_assign         steps/PolymerAssignmentStep.py:24-32,84-129 (golden vectors:
                          tests/golden/make_golden_polymer.py, the reference run here)
 """
@@ -249,4 +250,22 @@ def polymer_assign(crd, loci, edges, prob, rng):
         d = np.linalg.norm(crd[i, :, :] - crd[i + 1, :, :], axis=1)
         idx = np.argsort(np.argsort(d, kind='stable'), kind='stable')
         out[q] = sampled[idx]
+    return out
+
+
+def contact_counts(crd, radii, contact_range):
+    """Population contact counts behind HicEvaluationStep.reduce's buildContactMap
+    (steps/HicEvaluationStep.py:109; alabtools, absent: parity unpinned) with IGM's
+    own contact test -- float32 norm (restraints/inter_hic.py:47) <= fl32(cr * fl32(ri + rj))
+    (restraints/hic.py r0).  crd (nbead, S, 3) float32.  Returns (nbead, nbead) int32."""
+    crd = np.asarray(crd, f32)
+    r = np.asarray(radii, f32)
+    thr = f32(contact_range) * (r[:, None] + r[None, :])
+    n = crd.shape[0]
+    out = np.zeros((n, n), np.int32)
+    for s in range(crd.shape[1]):
+        x = crd[:, s, :]
+        d = x[:, None, :] - x[None, :, :]
+        dd = np.sqrt((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2])
+        out += dd <= thr
     return out

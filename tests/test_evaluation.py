@@ -1,0 +1,90 @@
+"""Hi-C evaluation (HicEvaluationStep.reduce, igm/steps/HicEvaluationStep.py:96-179):
+the GPU population contact map against the oracle (bit-exact counts), and the score
+arithmetic against a literal restatement of reduce()'s dict/coo loop.  buildContactMap
+and sumCopies are alabtools' (absent here): their parity is unpinned, see
+igm_amd/evaluation.py."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle.asteps as OA
+from igm_amd import evaluation as EV
+
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+@pytest.fixture(scope='module')
+def pop():
+    return np.load(os.path.join(GOLD, 'demo_population.npz'))
+
+
+def test_oracle_counts_match_scalar_loop():
+    rng = np.random.default_rng(3)
+    crd = (rng.standard_normal((9, 5, 3)) * 300).astype(np.float32)
+    r = rng.uniform(80, 160, 9).astype(np.float32)
+    o = OA.contact_counts(crd, r, 2.0)
+    for i in range(9):
+        for j in range(9):
+            n = 0
+            for s in range(5):
+                d = crd[i, s] - crd[j, s]
+                dd = np.sqrt(np.float32(np.float32(d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]))
+                n += int(dd <= np.float32(2.0) * np.float32(r[i] + r[j]))
+            assert o[i, j] == n
+    assert (np.diag(o) == 5).all() and (o == o.T).all()
+
+
+def test_sum_copies_and_score_follow_reduce():
+    full = np.arange(16, dtype=np.float64).reshape(4, 4) / 40
+    full = full + full.T
+    copy_ptr = np.array([0, 2, 4])
+    copy_idx = np.array([0, 2, 1, 3])  # haploid 0 = beads 0, 2; haploid 1 = beads 1, 3
+    h = EV.sum_copies(full, copy_ptr, copy_idx)
+    assert h[0, 1] == full[0, 1] + full[0, 3] + full[2, 1] + full[2, 3]
+    assert h[1, 1] == full[1, 1] + full[1, 3] + full[3, 1] + full[3, 3]
+    rng = np.random.default_rng(5)
+    inp = np.triu(rng.uniform(0, 0.5, (12, 12)))
+    out = np.clip(inp + rng.normal(0, 0.05, (12, 12)), 0, 1) * (rng.uniform(size=(12, 12)) > 0.2)
+    sigma = 0.1
+    # reduce(): dict of input pairs i != j with p >= sigma; loop over stored output entries
+    want = {(i, j): inp[i, j] for i in range(12) for j in range(i, 12) if inp[i, j] >= sigma and i != j}
+    diffs, rel = [], []
+    for i in range(12):
+        for j in range(i, 12):
+            if out[i, j] != 0 and (i, j) in want:
+                diffs.append(out[i, j] - want[i, j])
+                rel.append((out[i, j] - want[i, j]) / want[i, j])
+    score, ad, ar, n = EV.hic_evaluation(inp, out, sigma)
+    assert n == len(diffs)
+    assert score == np.abs(np.array(rel)).mean()
+    assert ad == np.average(diffs) and ar == np.average(rel)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('nbead,S', [(1, 1), (130, 37), (600, 100)])
+def test_gpu_contact_counts_match_oracle(pop, nbead, S):
+    crd = np.ascontiguousarray(pop['coordinates'][:nbead, :S])
+    r = pop['radii'][:nbead]
+    got = EV.contact_counts(crd, r, 2.0 * (1 + EV.EPS))
+    assert got.tobytes() == OA.contact_counts(crd, r, 2.0 * (1 + EV.EPS)).tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_contact_map_full_population(pop):
+    crd, r = pop['coordinates'], pop['radii']
+    S = crd.shape[1]
+    got = EV.contact_counts(crd, r, 2.0)
+    assert (got == got.T).all() and (np.diag(got) == S).all() and got.min() >= 0 and got.max() <= S
+    rows = np.array([0, 1, 777, 1503, 1504, 3007])  # the whole oracle is 3008^2 x 100: check rows
+    for i in rows:
+        x = crd[i][None]  # (1, S, 3)
+        d = x - crd
+        dd = np.sqrt((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2])
+        ref = (dd <= np.float32(2.0) * (r[i] + r)[:, None]).sum(axis=1)
+        assert np.array_equal(got[i], ref.astype(np.int32))
+    m = EV.contact_map(crd, r, 2.0, pop['copy_ptr'], pop['copy_idx'])
+    nhap = len(pop['copy_ptr']) - 1
+    assert m.shape == (nhap, nhap) and m.min() >= 0 and m.max() <= 1
+    # neighbouring beads of a chain are in contact in (nearly) every structure
+    assert np.median(np.diag(m, 1)) == 1.0
