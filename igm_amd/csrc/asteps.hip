@@ -1057,13 +1057,27 @@ extern "C" int igm_polymer_assign(igm_ctx* c, uint32_t flags, const float* xyz, 
 // Hi-C map of the population with alabtools' HssFile.buildContactMap(contactRange) (:109)
 // before summing the copies.  counts[i, j] = the number of structures with
 // |x_i - x_j| <= fl32(contact_range * fl32(r_i + r_j)), the float32 norm of the A/M
-// contact test (inter_hic.py:47) against the Hi-C restraint's r0 (hic.py).  One
+// contact test (inter_hic.py:47) against the Hi-C restraint's r0 (hic.py), decided
+// exactly on the squared norm (sq_bound).  One
 // workgroup per 64x64 bead tile (upper triangle, mirrored on store); the structures
 // stream through LDS in chunks of kCS, each thread keeps a 4x4 block of counters.
 namespace {
 constexpr int kCT = 64;  // beads per tile side
 constexpr int kCS = 32;  // structures per LDS chunk
 constexpr int kCRow = kCS * 3 + 1;  // padded LDS row (floats)
+
+// The largest float T with  RN(sqrt(d2)) <= dist  <=>  d2 <= T  for every float d2 >= 0
+// (sqrt_le's exact bound (dist + ulp/2)^2, rounded down to the float strictly below it):
+// the per-structure test is then the float32 squared norm and one compare, no sqrt.
+__device__ __forceinline__ float sq_bound(float dist) {
+    if (!(dist >= 0.0f)) return -1.0f;
+    if (isinf(dist)) return INFINITY;
+    const double m = (double)dist + 0.5 * ((double)nextafterf(dist, INFINITY) - (double)dist);
+    const double M = m * m;  // exact (m has <= 25 significant bits)
+    float t = (float)M;
+    if ((double)t >= M) t = nextafterf(t, -INFINITY);
+    return t;
+}
 
 __global__ void __launch_bounds__(kBT) contact_map_kernel(const float* __restrict__ xyz, int n, int S,
                                                           const float* __restrict__ radii, float cr,
@@ -1082,7 +1096,7 @@ __global__ void __launch_bounds__(kBT) contact_map_kernel(const float* __restric
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const int j = min(j0 + tj * 4 + b, n - 1);
-            thr[a][b] = __fmul_rn(cr, __fadd_rn(radii[i], radii[j]));
+            thr[a][b] = sq_bound(__fmul_rn(cr, __fadd_rn(radii[i], radii[j])));
             cnt[a][b] = 0;
         }
     }
@@ -1100,6 +1114,7 @@ __global__ void __launch_bounds__(kBT) contact_map_kernel(const float* __restric
             lj[r * kCRow + c] = vj;
         }
         __syncthreads();
+#pragma unroll 1
         for (int s = 0; s < ns; ++s) {
             float xi[4][3], xj[4][3];
 #pragma unroll
@@ -1113,9 +1128,10 @@ __global__ void __launch_bounds__(kBT) contact_map_kernel(const float* __restric
             for (int a = 0; a < 4; ++a)
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
-                    const float d = norm3(__fsub_rn(xi[a][0], xj[b][0]), __fsub_rn(xi[a][1], xj[b][1]),
-                                          __fsub_rn(xi[a][2], xj[b][2]));
-                    cnt[a][b] += d <= thr[a][b];
+                    const float dx = __fsub_rn(xi[a][0], xj[b][0]), dy = __fsub_rn(xi[a][1], xj[b][1]),
+                                dz = __fsub_rn(xi[a][2], xj[b][2]);
+                    const float d2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+                    cnt[a][b] += d2 <= thr[a][b];
                 }
         }
     }
