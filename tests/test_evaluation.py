@@ -88,3 +88,23 @@ def test_gpu_contact_map_full_population(pop):
     assert m.shape == (nhap, nhap) and m.min() >= 0 and m.max() <= 1
     # neighbouring beads of a chain are in contact in (nearly) every structure
     assert np.median(np.diag(m, 1)) == 1.0
+
+
+@pytest.mark.gpu
+def test_gpu_contact_counts_near_ties():
+    """Pairs within a few ulp of the contact threshold: the squared-norm bound of the
+    kernel must decide exactly as the float32 sqrt compare of the oracle."""
+    rng = np.random.default_rng(11)
+    S, nb = 256, 8
+    r = np.full(nb, 50.0, np.float32)
+    crd = np.zeros((nb, S, 3), np.float32)
+    base = rng.uniform(-3000, 3000, (S, 3)).astype(np.float32)
+    for b in range(nb):
+        u = rng.standard_normal((S, 3))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        scale = 200.0 * (1 + rng.integers(-40, 40, S) * 6e-8) * (b > 0)
+        crd[b] = (base + u * scale[:, None]).astype(np.float32)
+    got = EV.contact_counts(crd, r, 2.0)
+    ref = OA.contact_counts(crd, r, 2.0)
+    assert got.tobytes() == ref.tobytes()
+    assert 0 < ref[0, 1:].min() and ref[0, 1:].max() < S  # genuinely split decisions
