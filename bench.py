@@ -45,6 +45,11 @@ def parse():
     ap.add_argument('--sprite-clusters', type=int, default=20000, help='SPRITE clusters in the D/E measurement')
     ap.add_argument('--protocol-scale', type=float, default=1.0,
                     help='scale the MD step counts (only for smoke tests; the metric needs 1.0)')
+    ap.add_argument('--no-c', action='store_true', help='skip the config C (200 kb) block of the N=1 line')
+    ap.add_argument('--c-steps', type=int, default=1, help='timed A/M iterations of the config C block')
+    ap.add_argument('--c-warmup', type=int, default=1, help='warmup A/M iterations of the config C block')
+    ap.add_argument('--c-cpu-scale', type=float, default=0.02,
+                    help='protocol scale of the config C CPU-baseline sample (0: skip it)')
     a = ap.parse_args()
     if a.nstruct is None:
         a.nstruct = 1000 if a.config == 'B' else 125
@@ -100,6 +105,133 @@ def cpu_baseline(args, it, inp):
             'sample': '%d structures of config B (full demo protocol, same initial coordinates and Hi-C '
                       'restraints as GPU step 0), fp64 C restatement, one structure per thread, %.1f s'
                       % (n, dt)}
+
+
+def cpu_baseline_c(args, it, inp, nthreads):
+    """The fp64 C restatement (oracle/mstep_ref.c, kind 'port') on a bounded sample of
+    config C: one 200 kb structure per thread, same initial coordinates and Hi-C
+    restraints as the GPU's first step, the demo protocol with every MD step count
+    scaled by args.c_cpu_scale (the stage mix kept), timed once with and once without
+    the MD stages; the MD part is extrapolated to the full protocol and the CG part
+    added as measured: t = (t_sample - t_cg) / scale + t_cg per structure."""
+    import oracle
+    from igm_amd import model as M
+    from igm_amd._lib import bond_dtype
+    n = min(nthreads, it.S_local)
+    ptr = it.hic_ptr.cpu().numpy()
+    bonds = it.hic_bonds.cpu().numpy().view(bond_dtype)
+    sptr = ptr[:n + 1].copy()
+    sb = bonds[:sptr[-1]].copy()
+    x = inp['xyz'][:n].copy()
+    seeds = M.lammps_seeds(it.seed, np.arange(n), 0)
+    proto = json.loads(json.dumps(syn_protocol()))
+    cap = proto['custom_annealing_protocol']
+    sc = args.c_cpu_scale
+    cap['mdsteps'] = [max(1, int(round(k * sc))) for k in cap['mdsteps']]
+    cap['relax']['mdsteps'] = max(1, int(round(cap['relax']['mdsteps'] * sc)))
+    prm = M.params_from_cfg({'optimization': {'optimizer_options': proto}}, [((5500.0,) * 3, 1.0)])
+    t0 = time.perf_counter()
+    oracle.mstep_run(prm, x.copy(), inp['atoms'].radii, inp['atoms'].flags, inp['poly'], sptr, sb, seeds, nthreads=n)
+    t_sample = time.perf_counter() - t0
+    prm.nstages = 0  # CG only
+    t0 = time.perf_counter()
+    oracle.mstep_run(prm, x.copy(), inp['atoms'].radii, inp['atoms'].flags, inp['poly'], sptr, sb, seeds, nthreads=n)
+    t_cg = time.perf_counter() - t0
+    t_full = max(t_sample - t_cg, 0.0) / sc + t_cg
+    return {'value': n / t_full, 'unit': 'structures/s', 'cores': n, 'kind': 'port',
+            'sample': '%d structures of config C (200 kb, same initial coordinates and Hi-C restraints as GPU step 0), '
+                      'fp64 C restatement, one structure per thread; demo protocol MD steps x%g: %.1f s, CG alone '
+                      '%.1f s, extrapolated to the full protocol %.0f s per %d structures' % (n, sc, t_sample, t_cg,
+                                                                                          t_full, n)}
+
+
+def syn_protocol():
+    from igm_amd import synthetic as syn
+    return syn.DEMO_PROTOCOL
+
+
+def cpu_baseline_astep(args, it, nthreads, npairs=4000):
+    """The bit-exact C restatement of get_actdist (oracle/actdist_ref.c, kind 'port'),
+    OpenMP over pairs on `nthreads` host threads, on a seeded sample of the same pair
+    list and population as the GPU A-step; pairs/s."""
+    import oracle
+    from igm_amd._lib import pair_dtype
+    rng = np.random.default_rng(0)
+    P = it.npairs
+    sub = np.sort(rng.choice(P, min(npairs, P), replace=False))
+    pairs = it.pairs.cpu().numpy().view(pair_dtype)[sub]
+    xyz = it.pop_bm.cpu().numpy()
+    t0 = time.perf_counter()
+    oracle.actdist(xyz, it.bead_radii.cpu().numpy(), it.copy_ptr.cpu().numpy(), it.copy_idx.cpu().numpy(),
+                   it.hap_chrom.cpu().numpy(), pairs, float(it.cr), int(it.it_corr), nthreads=nthreads)
+    dt = time.perf_counter() - t0
+    return {'value': len(sub) / dt, 'unit': 'pairs/s', 'cores': nthreads, 'kind': 'port',
+            'sample': '%d seeded pairs of the same list, %d structures, %.2f s' % (len(sub), it.S_total, dt)}
+
+
+def bench_config_c(args, dev, ctx_threads):
+    """SURVEY 8(d) config C (BASELINE.json configs[2]): 200 kb diploid, the 125-structure
+    shard one GPU owns at 8 GPUs, Hi-C sigma 0.01, full demo protocol, inputs resident
+    in HBM; c_warmup + c_steps A/M iterations on this GPU alone.  Roofline of the
+    population engine: SURVEY 8(d)'s algorithmic bytes per force evaluation per
+    structure (76 N + 16 B) times the evaluations of the anneal, over the anneal's
+    HIP-event time (the five pop_* kernels of every MD step)."""
+    import torch
+    from igm_amd.pipeline import AMIteration
+    ca = argparse.Namespace(**vars(args))
+    ca.config, ca.nstruct, ca.sigma, ca.protocol_scale = 'C', 125, 0.01, 1.0
+    inp = build_inputs(ca, 0)
+    pop = inp['pop']
+    it = AMIteration(dev, inp['xyz'], inp['atoms'], inp['chrom'], pop['copy_ptr'], pop['copy_idx'], inp['pairs'],
+                     inp['prm'], inp['poly'], first_sid=0, rank=0, world=1)
+    cpu = None
+    if args.c_cpu_scale > 0:
+        it.astep()
+        it.select()
+        torch.cuda.synchronize(dev)
+        cpu = cpu_baseline_c(args, it, inp, ctx_threads)
+        it.xyz.copy_(torch.from_numpy(inp['xyz']).to(dev))
+        it.pairs.copy_(torch.from_numpy(np.ascontiguousarray(inp['pairs']).view(np.uint8)).to(dev))
+    for _ in range(args.c_warmup):
+        it.step()
+    torch.cuda.synchronize(dev)
+    anneal_ms, bytes_launch = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.c_steps):
+        tm = it.step()
+        anneal_ms.append(it.ctx.kernel_ms('anneal'))
+        bytes_launch.append(it.algorithmic_anneal_bytes())
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    a_ms = float(np.mean(anneal_ms))
+    achieved = float(np.mean(bytes_launch)) / (a_ms * 1e-3) / 1e9
+    info = it.info_host()
+    traffic, traffic_src = measured_traffic('C')
+    out = {
+        'metric': 'M-step structures/sec + A/M iteration wall-time, 200 kb diploid, the 125-structure shard of '
+                  'pop=1000 at 8 GPUs (configs[2]) on 1 GPU',
+        'value': it.S_local * args.c_steps / dt, 'unit': 'structures/s', 'steps': args.c_steps,
+        'warmup': args.c_warmup, 'ms_per_step': 1000.0 * dt / args.c_steps,
+        'config': {'workload': 'C: 200 kb diploid (29 838 beads), Hi-C only, 125 structures, demo protocol',
+                   'sigma': 0.01, 'npairs': int(it.npairs_total)},
+        'roofline': {'bound': 'hbm', 'kernel': 'population engine (pop_integrate, pop_sort, pop_permute, pop_fill, '
+                                               'pop_force per MD step)',
+                     'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                     'traffic': traffic, 'traffic_source': traffic_src,
+                     'algorithmic_bytes_per_launch': float(np.mean(bytes_launch)), 'avg_launch_ms': a_ms},
+        'cpu_baseline': cpu,
+        'breakdown': {'astep_ms': 1000 * tm['astep_s'], 'mstep_ms': 1000 * tm['mstep_s'], 'anneal_ms': a_ms,
+                      'cg_ms': it.ctx.kernel_ms('cg'), 'actdist_ms': it.ctx.kernel_ms('actdist'),
+                      'hic_select_ms': it.ctx.kernel_ms('hic_select'),
+                      'violation_score': it.violation_score(),
+                      'median_final_energy_per_bead': float(np.median(info['final_energy'])) / inp['atoms'].nbead,
+                      'rows': int(it.nrows), 'hic_bonds_per_struct': it.nbonds / it.S_local,
+                      'mean_rebuilds': float(np.mean(info['nrebuild']))},
+        'excludes': 'host pair enumeration (select_pairs) and file I/O: inputs resident in HBM',
+    }
+    del it
+    torch.cuda.empty_cache()
+    return out
 
 
 def bench_asteps_de(args, ctx):
@@ -224,15 +356,20 @@ def main():
         mstep_s.append(tm['mstep_s'])
     barrier()
     dt = time.perf_counter() - t0
+    kms = {k: it.ctx.kernel_ms(k) for k in ('cg', 'actdist', 'hic_select', 'violations')}  # before the C block
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    de = None
+    de = cblock = astep_cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        astep_cpu = cpu_baseline_astep(args, it, args.cpu_threads)
     if rank == 0 and world == 1 and not args.no_de:  # the N=1 line carries it; scaling runs stay lean
         de = bench_asteps_de(args, it.ctx)
     score = it.violation_score()
     info = it.info_host()
+    if rank == 0 and world == 1 and args.config == 'B' and not args.no_c:
+        cblock = bench_config_c(args, dev, args.cpu_threads)
     ms_per_step = 1000.0 * dt / max(args.steps, 1)
     total = it.S_local * world
     value = total * args.steps / dt
@@ -261,15 +398,19 @@ def main():
                          'algorithmic_bytes_per_launch': float(np.mean(bytes_launch)),
                          'avg_launch_ms': a_ms},
             'cpu_baseline': cpu,
+            'cpu_baseline_astep': astep_cpu,
+            'astep_pairs_per_s': float(it.npairs) / (kms['actdist'] * 1e-3),
+            'config_C': cblock,
             'asteps_DE': de,
             'breakdown': {'astep_ms': 1000 * float(np.mean(astep_s)), 'mstep_ms': 1000 * float(np.mean(mstep_s)),
-                          'anneal_ms': a_ms, 'cg_ms': it.ctx.kernel_ms('cg'),
-                          'actdist_ms': it.ctx.kernel_ms('actdist'), 'hic_select_ms': it.ctx.kernel_ms('hic_select'),
-                          'violations_ms': it.ctx.kernel_ms('violations'),
+                          'anneal_ms': a_ms, 'cg_ms': kms['cg'],
+                          'actdist_ms': kms['actdist'], 'hic_select_ms': kms['hic_select'],
+                          'violations_ms': kms['violations'],
                           'violation_score': score, 'median_final_energy_per_bead':
                               float(np.median(info['final_energy'])) / inp['atoms'].nbead,
                           'rows': int(it.nrows), 'hic_bonds_per_struct': it.nbonds / it.S_local,
                           'mean_rebuilds': float(np.mean(info['nrebuild']))},
+            'excludes': 'host pair enumeration (select_pairs) and file I/O: inputs resident in HBM',
         }
         if os.environ.get('IGM_PROF'):
             line['profile'] = it.ctx.mstep_profile()

@@ -118,6 +118,7 @@ SIGNATURES = {
     'igm_fish_assign': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp,
                                _vp, _vp]),
     'igm_contact_map': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _f64, _vp]),
+    'igm_contact_map_haploid': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _f64, _vp, _vp, _i32, _vp]),
     'igm_polymer_assign': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
     'igm_sprite_assign': (_i32, [_vp, _u32, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32,
                                  _vp, _vp, _vp, _vp]),

@@ -1079,9 +1079,15 @@ __device__ __forceinline__ float sq_bound(float dist) {
     return t;
 }
 
+// HAP: the copies are summed on the device -- counts is (nhap, nhap) and every pair
+// (i, j) adds its count to (hap_of[i], hap_of[j]) and (hap_of[j], hap_of[i]) (integer
+// atomics: the sum is exact and order-independent); diagonal tiles take each unordered
+// pair once.
+template <bool HAP>
 __global__ void __launch_bounds__(kBT) contact_map_kernel(const float* __restrict__ xyz, int n, int S,
                                                           const float* __restrict__ radii, float cr,
-                                                          int* __restrict__ counts) {
+                                                          int* __restrict__ counts, const int* __restrict__ hap_of,
+                                                          int nhap) {
     const int bi = blockIdx.y, bj = blockIdx.x;
     if (bj < bi) return;  // upper-triangle tiles only (whole workgroup exits together)
     __shared__ float li[kCT * kCRow];
@@ -1143,6 +1149,13 @@ __global__ void __launch_bounds__(kBT) contact_map_kernel(const float* __restric
         for (int b = 0; b < 4; ++b) {
             const int j = j0 + tj * 4 + b;
             if (j >= n) continue;
+            if (HAP) {
+                if (j < i || cnt[a][b] == 0) continue;  // diagonal tiles: each unordered pair once
+                const size_t ha = (size_t)hap_of[i], hb = (size_t)hap_of[j];
+                atomicAdd(&counts[ha * nhap + hb], cnt[a][b]);
+                if (i != j) atomicAdd(&counts[hb * nhap + ha], cnt[a][b]);
+                continue;
+            }
             counts[(size_t)i * n + j] = cnt[a][b];
             counts[(size_t)j * n + i] = cnt[a][b];
         }
@@ -1166,10 +1179,53 @@ extern "C" int igm_contact_map(igm_ctx* c, uint32_t flags, const float* xyz, int
     IGM_TRY(out_device(c, flags, "cm_counts", counts, (size_t)nbead * nbead, &d_cnt));
     {
         Timed tm(c, "contact_map");
-        hipLaunchKernelGGL(contact_map_kernel, dim3((unsigned)nt, (unsigned)nt), dim3(kBT), 0, c->stream, d_xyz,
-                           (int)nbead, (int)nstruct, d_radii, (float)contact_range, (int*)d_cnt);
+        hipLaunchKernelGGL(contact_map_kernel<false>, dim3((unsigned)nt, (unsigned)nt), dim3(kBT), 0, c->stream,
+                           d_xyz, (int)nbead, (int)nstruct, d_radii, (float)contact_range, (int*)d_cnt,
+                           (const int*)nullptr, 0);
         IGM_HIP_CHECK(c, hipGetLastError());
     }
     IGM_TRY(to_host(c, flags, counts, d_cnt, (size_t)nbead * nbead));
+    return finish(c, flags);
+}
+
+extern "C" int igm_contact_map_haploid(igm_ctx* c, uint32_t flags, const float* xyz, int32_t nbead, int32_t nstruct,
+                                       const float* radii, double contact_range, const int32_t* copy_ptr,
+                                       const int32_t* copy_idx, int32_t nhap, int32_t* counts) {
+    if (!c) return IGM_E_INVALID;
+    if (nbead <= 0 || nstruct <= 0 || nhap <= 0 || !xyz || !radii || !copy_ptr || !copy_idx || !counts ||
+        !(contact_range >= 0.0))
+        return fail(c, IGM_E_INVALID, "igm_contact_map_haploid: invalid arguments");
+    const int nt = (int)ceil_div(nbead, kCT);
+    if (nt > 65535) return fail(c, IGM_E_UNSUPPORTED, "igm_contact_map_haploid: %d beads exceed the tile grid", nbead);
+    IGM_HIP_CHECK(c, hipSetDevice(c->device));
+    // the haploid locus of every bead from the CSR copy index (host pointers)
+    std::vector<int32_t> hap(nbead, -1);
+    if (copy_ptr[0] != 0) return fail(c, IGM_E_INVALID, "igm_contact_map_haploid: copy_ptr[0] != 0");
+    for (int a = 0; a < nhap; ++a)
+        for (int k = copy_ptr[a]; k < copy_ptr[a + 1]; ++k) {
+            const int b = copy_idx[k];
+            if (b < 0 || b >= nbead || hap[b] >= 0)
+                return fail(c, IGM_E_INVALID, "igm_contact_map_haploid: copy index entry %d invalid or repeated", b);
+            hap[b] = a;
+        }
+    for (int b = 0; b < nbead; ++b)
+        if (hap[b] < 0) return fail(c, IGM_E_INVALID, "igm_contact_map_haploid: bead %d has no haploid locus", b);
+    const float* d_xyz;
+    const float* d_radii;
+    const int32_t* d_hap;
+    IGM_TRY(to_device(c, flags, "cm_xyz", xyz, (size_t)nbead * nstruct * 3, &d_xyz));
+    IGM_TRY(to_device(c, flags, "cm_radii", radii, (size_t)nbead, &d_radii));
+    IGM_TRY(to_device(c, 0u, "cm_hap", hap.data(), (size_t)nbead, &d_hap));
+    int32_t* d_cnt;
+    IGM_TRY(out_device(c, flags, "cm_counts", counts, (size_t)nhap * nhap, &d_cnt));
+    IGM_HIP_CHECK(c, hipMemsetAsync(d_cnt, 0, sizeof(int32_t) * (size_t)nhap * nhap, c->stream));
+    {
+        Timed tm(c, "contact_map");
+        hipLaunchKernelGGL(contact_map_kernel<true>, dim3((unsigned)nt, (unsigned)nt), dim3(kBT), 0, c->stream,
+                           d_xyz, (int)nbead, (int)nstruct, d_radii, (float)contact_range, (int*)d_cnt, d_hap,
+                           (int)nhap);
+        IGM_HIP_CHECK(c, hipGetLastError());
+    }
+    IGM_TRY(to_host(c, flags, counts, d_cnt, (size_t)nhap * nhap));
     return finish(c, flags);
 }

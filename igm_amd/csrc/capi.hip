@@ -38,6 +38,12 @@ void igm_ctx_destroy(igm_ctx* c) {
         if (kv.second.first) (void)hipEventDestroy(kv.second.first);
         if (kv.second.second) (void)hipEventDestroy(kv.second.second);
     }
+    for (size_t g = 0; g < c->aux.size(); ++g) {
+        (void)hipStreamSynchronize(c->aux[g]);
+        (void)hipStreamDestroy(c->aux[g]);
+        (void)hipEventDestroy(c->aux_ev[g]);
+    }
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

@@ -25,6 +25,11 @@ struct igm_ctx {
     int vol_nmap = 0, vol_nsmap = 0;
     int num_cus = 256;
     size_t lds_per_block = 65536;
+    // auxiliary streams (+ one event each) for independent work inside one call,
+    // created on first use: the population engine runs its structure groups on them
+    std::vector<hipStream_t> aux;
+    std::vector<hipEvent_t> aux_ev;
+    hipEvent_t fork_ev = nullptr;
 };
 
 namespace igm {
@@ -132,5 +137,35 @@ struct Timed {
 };
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// at least n auxiliary streams; the work on them is forked from and joined into c->stream
+inline int aux_streams(igm_ctx* c, int n) {
+    if (!c->fork_ev) IGM_HIP_CHECK(c, hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    while ((int)c->aux.size() < n) {
+        hipStream_t st;
+        hipEvent_t ev;
+        IGM_HIP_CHECK(c, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        IGM_HIP_CHECK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->aux.push_back(st);
+        c->aux_ev.push_back(ev);
+    }
+    return IGM_OK;
+}
+
+// the first n auxiliary streams wait for the work queued so far on c->stream
+inline int aux_fork(igm_ctx* c, int n) {
+    IGM_HIP_CHECK(c, hipEventRecord(c->fork_ev, c->stream));
+    for (int g = 0; g < n; ++g) IGM_HIP_CHECK(c, hipStreamWaitEvent(c->aux[g], c->fork_ev, 0));
+    return IGM_OK;
+}
+
+// c->stream waits for the work queued on the first n auxiliary streams
+inline int aux_join(igm_ctx* c, int n) {
+    for (int g = 0; g < n; ++g) {
+        IGM_HIP_CHECK(c, hipEventRecord(c->aux_ev[g], c->aux[g]));
+        IGM_HIP_CHECK(c, hipStreamWaitEvent(c->stream, c->aux_ev[g], 0));
+    }
+    return IGM_OK;
+}
 
 }  // namespace igm

@@ -52,7 +52,11 @@ constexpr int kLdsListSlots = 8;          // LDS path: the first slots of every 
 #ifndef IGM_PAIR_BATCH
 #define IGM_PAIR_BATCH 4
 #endif
-constexpr int kPopPairBatch = 8;  // HBM engine: neighbours per batch (more loads in flight, VGPRs allow it)
+#ifndef IGM_POP_PAIR_BATCH
+#define IGM_POP_PAIR_BATCH 8
+#endif
+constexpr int kPopPairBatch = IGM_POP_PAIR_BATCH;  // HBM engine: neighbours per batch (loads in flight together)
+
 // LDS anneal kernel: neighbours per batch.  LDS latency is short and lists are short, so
 // the masked tail of a wide batch costs more than the extra loads in flight win
 // (measured config B, anneal: batch 2 1700 ms, 1 1761 ms, 4 1779 ms, 8 1907 ms)
@@ -303,7 +307,10 @@ __device__ __forceinline__ void walk27(int c, const OffT* cell, const uint16_t* 
             for (int q = beg; q < end; q += WB) {
                 int jj[WB];
 #pragma unroll
-                for (int u = 0; u < WB; ++u) jj[u] = (int)sorted[q + u < end ? q + u : beg];
+                for (int u = 0; u < WB; ++u) {
+                    const int qq = q + u < end ? q + u : beg;
+                    jj[u] = sorted ? (int)sorted[qq] : qq;  // no `sorted`: the runs hold the ids themselves
+                }
 #pragma unroll
                 for (int u = 0; u < WB; ++u) f(jj[u], q + u < end);
             }
@@ -870,79 +877,103 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
 }
 
 // ------------------------------------------------------------- population engine
-// Structures too large for one CU's LDS (the 200 kb model, 29 838 beads) are run as
-// ONE system: every step is a handful of launches over all atoms of all structures
-// (full-chip occupancy, memory-level parallelism), each structure keeping its own
-// HBM Verlet list, cell grid and temperature.  Blocks never straddle structures:
-// block b -> structure b / nbs, atoms (b % nbs) * kPopBS + t.  Per-structure sums
-// (temperature) go through per-block partials summed in a fixed order, so a run is
-// bitwise reproducible.
+// Structures too large for one CU's LDS (the 200 kb model, 29 838 beads) run as ONE
+// system: a step is a few launches over all atoms of all structures.  Every
+// structure keeps its per-atom state in SLOT order -- the order of its atoms in the
+// cell grid of its last Verlet-list build (cells x-fastest, ascending atom ids inside
+// a cell, non-bead atoms last) -- so the 27-cell walk of a build reads contiguous
+// position runs, and the neighbour and bond-partner gathers of a wave of 64
+// consecutive slots fall on a few nearby cache lines.  At every build the state is
+// permuted into the new slot order (two buffers) and the structure's bonds are
+// re-indexed into slot space.  Per MD step:
+//   pop_integrate  rescale of the previous step, kick, drift, displacement check, bbox
+//   pop_sort       flagged structures, one workgroup each: counting sort into the cell
+//                  grid in LDS, ids sorted inside each cell (deterministic), slot map
+//   pop_permute    flagged structures: state and bonds into the new slot order
+//   pop_fill       flagged structures: Verlet list (slot ids) from the cell runs
+//   pop_force      forces, final kick, per-block kinetic-energy partial
+// The three build kernels exit at once when no structure is flagged.  Per-structure
+// sums go through per-block partials added in a fixed order, so a run is bitwise
+// reproducible.
 constexpr int kPopBS = 256;
+constexpr int kPopSortNT = 1024;
+constexpr int kPopCells = kCellCapBig + 2;  // cell offsets of a structure: real cells, non-bead run, end
+
+struct PopBuf {
+    float4* pos;   // (B, ldn): x, y, z, w = radius (bead) or -(radius + 1)
+    float4* vel;   // (B, ldn): vx, vy, vz, w = the atom flags (bit pattern)
+    float4* frc;   // (B, ldn)
+    int* aid;      // (B, ldn) atom id of a slot
+    int* slot;     // (B, ldn) slot of an atom id
+};
 
 struct PopArgs {
     Common cm;
     DevParams P;
-    unsigned char* ws;  // per structure: NList arrays + float4 positions (carve_ws)
-    size_t ws_stride;
-    float4* v4;         // (B, ldn)
-    float4* f4;         // (B, ldn)
-    float4* xb4;        // (B, ldn) positions at the last list build
-    float* gp;          // (B, 8) grid lo[3], inv[3]
-    int* gn;            // (B, 8) grid nb[3]
-    int* flag;          // (B) list rebuild needed
-    int* nrebuild;      // (B)
-    double* kep;        // (B, nbs) per-block kinetic-energy partials (2x KE, mass 1)
-    float* bbp;         // (B, nbs, 6) per-block bounding-box partials {max -x, -y, -z, max x, y, z}
-    int* ncell;         // (B) cells of the structure's current grid
-    const double* dofs; // (B) dof of group nonfixed
+    PopBuf buf[2];
+    int* par;            // (B) buffer holding the current slot order
+    float4* xb;          // (B, ldn) position of the slot at its list build
+    uint16_t* nl;        // (B, nslice, kcap, 64) Verlet list, slot ids
+    uint16_t* nnb;       // (B, ldn) list length, or kNnbWalk
+    int* cell;           // (B, kPopCells) first slot of every cell of the build grid
+    float* gp;           // (B, 8) grid lo[3], inv[3]
+    int* gn;             // (B, 8) grid nb[3]
+    uint32_t* bent;      // (B, nslice, bdmax, 64) bonds of a slot: partner slot | type << 16 | lower << 31
+    uint16_t* bdeg;      // (B, ldn)
+    int bdmax;
+    int* flag;           // (B) list rebuild needed
+    int* flist;          // (B) the flagged structures of this step, compacted
+    int* nflag;          // (1)
+    int* nrebuild;       // (B)
+    double* kep;         // (B, nbs) per-block kinetic-energy partials (2x KE, mass 1)
+    float* bbp;          // (B, nbs, 6) per-block bounding boxes {max -x, -y, -z, max x, y, z}
+    const double* dofs;  // (B) dof of group nonfixed
     int nbs;
 };
 
-__device__ __forceinline__ NList<float, int> pop_list(const PopArgs& A, int s, BigWs<float>* W) {
-    NList<float, int> L;
-    carve_ws<float>(A.ws + (size_t)s * A.ws_stride, A.cm.natom, A.cm.ldn, A.cm.kcap, kCellCapBig, true, false, &L, W);
-    L.gp = A.gp + (size_t)s * 8;
-    L.gn = A.gn + (size_t)s * 8;
-    return L;
-}
-
-// XCD-aware block order: the grid (padded to a multiple of 8) is dealt round-robin
-// over the 8 XCDs, so logical block = (x % 8) * (grid / 8) + x / 8 keeps the blocks
-// of a structure on one XCD and its positions/lists in that XCD's L2.
-__device__ __forceinline__ int pop_block(const PopArgs& A) {
+// XCD-aware block order for the kernels over every structure: the grid (padded to a
+// multiple of 8) is dealt round-robin over the 8 XCDs, so logical block
+// (x % 8) * (grid / 8) + x / 8 keeps the blocks of a structure on one XCD and its
+// positions and lists in that XCD's L2.
+__device__ __forceinline__ int pop_block() {
     const int x = blockIdx.x, per = gridDim.x >> 3;
     return (x & 7) * per + (x >> 3);
 }
 
 __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float* xyz) {
-    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    const int lb = pop_block(), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
-    BigWs<float> W;
-    pop_list(A, s, &W);
+    if (lb == 0 && threadIdx.x == 0) *A.nflag = 0;
     if (a == 0) {
         A.flag[s] = 1;
         A.nrebuild[s] = 0;
+        A.par[s] = 0;
     }
     if (a >= A.cm.natom) return;
     const size_t i = (size_t)s * A.cm.ldn + a;
     const float* x = xyz + ((size_t)s * A.cm.natom + a) * 3;
     const uint32_t fl = A.cm.aflags[(size_t)s * A.cm.afs + a];
     const float r = A.cm.radii[a];
-    W.pos[a] = make_float4(x[0], x[1], x[2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
-    A.v4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    A.f4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const PopBuf& B = A.buf[0];
+    B.pos[i] = make_float4(x[0], x[1], x[2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
+    B.vel[i] = make_float4(0.f, 0.f, 0.f, __uint_as_float(fl));
+    B.frc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    B.aid[i] = a;
+    B.slot[i] = a;
     const float inf = __int_as_float(0x7f800000);
-    A.xb4[i] = make_float4(inf, inf, inf, 0.f);
+    A.xb[i] = make_float4(inf, inf, inf, 0.f);
 }
 
-// velocities of a run: 'velocity create' of segment seg (vsrc = vinit + seg stride) or given
+// velocities of a run: 'velocity create' of segment seg (vsrc = vinit + seg stride) or
+// given, in atom order
 __global__ void __launch_bounds__(kPopBS) pop_setvel_kernel(PopArgs A, const float* vsrc, size_t sstride) {
-    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
-    if (s >= A.cm.nstruct) return;
-    if (a >= A.cm.natom) return;
-    const float* v = vsrc + (size_t)s * sstride + (size_t)a * 3;
-    const bool mob = !(A.cm.aflags[(size_t)s * A.cm.afs + a] & IGM_ATOM_FIXED);
-    A.v4[(size_t)s * A.cm.ldn + a] = mob ? make_float4(v[0], v[1], v[2], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int lb = pop_block(), s = lb / A.nbs, i = (lb % A.nbs) * kPopBS + threadIdx.x;
+    if (s >= A.cm.nstruct || i >= A.cm.natom) return;
+    const PopBuf& B = A.buf[A.par[s]];
+    const size_t k = (size_t)s * A.cm.ldn + i;
+    const float* v = vsrc + (size_t)s * sstride + (size_t)B.aid[k] * 3;
+    const float w = B.vel[k].w;  // the flags
+    B.vel[k] = (__float_as_uint(w) & IGM_ATOM_FIXED) ? make_float4(0.f, 0.f, 0.f, w) : make_float4(v[0], v[1], v[2], w);
 }
 
 struct PopStep {
@@ -954,34 +985,38 @@ struct PopStep {
 };
 
 // temp/rescale factor of structure s at the end of step P.prev (fixed-order sum of partials)
+// (wave 0 loads the partials in parallel and adds them in a fixed tree: every block
+// gets the same bits, and no block waits on a serial chain of nbs loads)
 __device__ __forceinline__ float pop_factor(const PopArgs& A, const PopStep& S, int s, float* shared) {
-    if (threadIdx.x == 0) {
-        double ke = 0.0;
+    if (threadIdx.x < 64) {
         const double* kp = A.kep + (size_t)s * A.nbs;
-        for (int i = 0; i < A.nbs; ++i) ke += kp[i];
-        *shared = temp_rescale_factor(ke, A.dofs[s], S.prev, S.nsteps, S.t0, S.t1, S.window, S.fraction);
+        double ke = 0.0;
+        for (int i = threadIdx.x; i < A.nbs; i += 64) ke += kp[i];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) ke += __shfl_xor(ke, off);
+        if (threadIdx.x == 0)
+            *shared = temp_rescale_factor(ke, A.dofs[s], S.prev, S.nsteps, S.t0, S.t1, S.window, S.fraction);
     }
     __syncthreads();
     return *shared;
 }
 
 // [end_of_step rescale of the previous step] + initial_integrate + the displacement check
-__global__ void __launch_bounds__(kPopBS) pop_kick_drift_kernel(PopArgs A, PopStep S) {
+__global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopStep S) {
     __shared__ float fac;
     __shared__ float red[kPopBS / 64 * 6];
-    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    const int lb = pop_block(), s = lb / A.nbs, i = (lb % A.nbs) * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
     const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
-    BigWs<float> W;
-    pop_list(A, s, &W);
+    const PopBuf& B = A.buf[A.par[s]];
     int moved = 0;
     float mm[6] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
-    if (a < A.cm.natom) {
-        const size_t i = (size_t)s * A.cm.ldn + a;
-        float4 p = W.pos[a];
-        if (S.integrate && !(A.cm.aflags[(size_t)s * A.cm.afs + a] & IGM_ATOM_FIXED)) {
-            float4 v = A.v4[i];
-            const float4 f = A.f4[i];
+    if (i < A.cm.natom) {
+        const size_t k = (size_t)s * A.cm.ldn + i;
+        float4 p = B.pos[k];
+        float4 v = B.vel[k];
+        if (S.integrate && !(__float_as_uint(v.w) & IGM_ATOM_FIXED)) {
+            const float4 f = B.frc[k];
             v.x *= factor;
             v.y *= factor;
             v.z *= factor;
@@ -989,11 +1024,11 @@ __global__ void __launch_bounds__(kPopBS) pop_kick_drift_kernel(PopArgs A, PopSt
             p.x += S.dtv * v.x;
             p.y += S.dtv * v.y;
             p.z += S.dtv * v.z;
-            A.v4[i] = v;
-            W.pos[a] = p;
+            B.vel[k] = v;
+            B.pos[k] = p;
         }
         if (p.w >= 0.0f) {
-            const float4 b = A.xb4[i];
+            const float4 b = A.xb[k];
             const float dx = p.x - b.x, dy = p.y - b.y, dz = p.z - b.z;
             moved = !(dx * dx + dy * dy + dz * dz <= S.trig);
             mm[0] = -p.x;
@@ -1021,22 +1056,43 @@ __global__ void __launch_bounds__(kPopBS) pop_kick_drift_kernel(PopArgs A, PopSt
     }
 }
 
-// ---- population-wide Verlet-list build of the flagged structures (the steps of
-// build_nlist, each over all atoms / cells of every flagged structure):
-//   grid (+ zero counts) | count | scan | scatter | per-cell sort | fill
-__global__ void __launch_bounds__(256) pop_grid_kernel(PopArgs A) {
-    __shared__ int nc;
-    const int s = blockIdx.x;
+// One workgroup per flagged structure: the cell grid of build_nlist (cells of side >=
+// cut_list, at most kCellCapBig) from the bbox partials, then a counting sort of the
+// slots into it -- cell counts as packed u16 pairs in LDS, and with IDS_LDS the new
+// order of atom ids too (u16), so the ranks, the scan and the per-cell insertion
+// sort (ascending ids: deterministic) never leave the CU.  Non-bead atoms form a last
+// run after the real cells.  Writes the new slot order (aid, slot) and the cell
+// offsets, and flips the structure's parity.
+template <bool IDS_LDS>
+__global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t cw[];  // (kPopCells + 1) / 2 words, then ids
+    __shared__ int wsum[kMaxWaves];
+    __shared__ float sg[6];
+    __shared__ int sn[3];
+    const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (!A.flag[s]) return;
-    if (threadIdx.x == 0) {
+    const int N = A.cm.natom;
+    const size_t base = (size_t)s * A.cm.ldn;
+    const int p = A.par[s], q = p ^ 1;
+    const float4* pos = A.buf[p].pos + base;
+    const int* aido = A.buf[p].aid + base;
+    int* aidn = A.buf[q].aid + base;
+    int* slotn = A.buf[q].slot + base;  // first the packed (cell, rank) of every old slot
+    __shared__ float smm[6];
+    if (w < 6) {  // the structure's bbox from the blocks' partials, one wave per component
+        const float* bp = A.bbp + (size_t)s * A.nbs * 6;
+        float m = -3.0e38f;
+        for (int b = lane; b < A.nbs; b += 64) m = fmaxf(m, bp[b * 6 + w]);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        if (lane == 0) smm[w] = m;
+    }
+    __syncthreads();
+    if (t == 0) {
+        A.flist[atomicAdd(A.nflag, 1)] = s;
         float mm[6];
 #pragma unroll
-        for (int d = 0; d < 6; ++d) mm[d] = -3.0e38f;
-        const float* bp = A.bbp + (size_t)s * A.nbs * 6;
-        for (int b = 0; b < A.nbs; ++b)
-#pragma unroll
-            for (int d = 0; d < 6; ++d) mm[d] = fmaxf(mm[d], bp[b * 6 + d]);
-        // the grid of build_nlist: cells of side >= cut_list, at most kCellCapBig
+        for (int d = 0; d < 6; ++d) mm[d] = smm[d];
         float ext[3], vol = 1.0f;
         const float cut = A.P.cut_list;
 #pragma unroll
@@ -1049,141 +1105,313 @@ __global__ void __launch_bounds__(256) pop_grid_kernel(PopArgs A) {
         if (vol / (cs * cs * cs) > (float)kCellCapBig) cs = cbrtf(vol / (float)kCellCapBig) * 1.0001f;
         float* gp = A.gp + (size_t)s * 8;
         int* gn = A.gn + (size_t)s * 8;
-        int n = 1;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             int nbd = (int)floorf(ext[d] / cs);
             if (nbd < 1) nbd = 1;
-            gp[d] = -mm[d];
-            gp[3 + d] = ext[d] > 0.0f ? (float)nbd / ext[d] : 0.0f;
+            sg[d] = -mm[d];
+            sg[3 + d] = ext[d] > 0.0f ? (float)nbd / ext[d] : 0.0f;
+            sn[d] = nbd;
+            gp[d] = sg[d];
+            gp[3 + d] = sg[3 + d];
             gn[d] = nbd;
-            n *= nbd;
         }
-        A.ncell[s] = n;
-        nc = n;
     }
     __syncthreads();
-    BigWs<float> W;
-    const NList<float, int> L = pop_list(A, s, &W);
-    for (int c = threadIdx.x; c <= nc; c += 256) L.scratch[c] = 0;
-}
-
-__global__ void __launch_bounds__(kPopBS) pop_count_kernel(PopArgs A) {
-    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
-    if (s >= A.cm.nstruct) return;
-    if (!A.flag[s] || a >= A.cm.natom) return;
-    BigWs<float> W;
-    const NList<float, int> L = pop_list(A, s, &W);
-    const float4 p = W.pos[a];
-    if (!(p.w >= 0.0f)) return;
-    int* cnt = L.scratch;
-    int* slot = cnt + A.ncell[s] + 1;
-    slot[a] = atomicAdd(&cnt[cell_index<float>(p.x, p.y, p.z, L.gp, L.gp + 3, L.gn)], 1);
-}
-
-__global__ void __launch_bounds__(1024) pop_scan_kernel(PopArgs A) {
-    __shared__ int wsum[kMaxWaves];
-    const int s = blockIdx.x;
-    if (!A.flag[s]) return;
-    BigWs<float> W;
-    const NList<float, int> L = pop_list(A, s, &W);
-    const int n = A.ncell[s];
-    block_scan<1024, int, int>(L.scratch, L.scratch, n, wsum);
-    for (int c = threadIdx.x; c <= n; c += 1024) L.cell[c] = L.scratch[c];
-}
-
-__global__ void __launch_bounds__(kPopBS) pop_scatter_kernel(PopArgs A) {
-    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
-    if (s >= A.cm.nstruct) return;
-    if (!A.flag[s] || a >= A.cm.natom) return;
-    BigWs<float> W;
-    const NList<float, int> L = pop_list(A, s, &W);
-    const float4 p = W.pos[a];
-    if (!(p.w >= 0.0f)) return;
-    const int* slot = L.scratch + A.ncell[s] + 1;
-    L.sorted[L.cell[cell_index<float>(p.x, p.y, p.z, L.gp, L.gp + 3, L.gn)] + slot[a]] = (uint16_t)a;
-}
-
-constexpr int kPopCellBlocks = kCellCapBig / 256;
-
-__global__ void __launch_bounds__(256) pop_cellsort_kernel(PopArgs A) {
-    const int s = blockIdx.x / kPopCellBlocks, c = (blockIdx.x % kPopCellBlocks) * 256 + threadIdx.x;
-    if (!A.flag[s] || c >= A.ncell[s]) return;
-    BigWs<float> W;
-    const NList<float, int> L = pop_list(A, s, &W);
-    const int beg = L.cell[c], end = L.cell[c + 1];
-    for (int i = beg + 1; i < end; ++i) {  // deterministic order inside the cell
-        const uint16_t v = L.sorted[i];
-        int k = i - 1;
-        while (k >= beg && L.sorted[k] > v) {
-            L.sorted[k + 1] = L.sorted[k];
-            --k;
+    const float lo[3] = {sg[0], sg[1], sg[2]}, inv[3] = {sg[3], sg[4], sg[5]};
+    const int nb[3] = {sn[0], sn[1], sn[2]};
+    const int ncell = nb[0] * nb[1] * nb[2];
+    const int nw = (ncell + 3) >> 1;  // words holding the cells 0..ncell+1
+    uint16_t* ids = reinterpret_cast<uint16_t*>(cw + ((kPopCells + 1) >> 1));
+    for (int k = t; k < nw; k += kPopSortNT) cw[k] = 0u;
+    __syncthreads();
+    constexpr int U = 4;  // independent loads in flight per thread
+    for (int i0 = t; i0 < N; i0 += U * kPopSortNT) {
+        float4 pp[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * kPopSortNT;
+            pp[u] = pos[i < N ? i : 0];
         }
-        L.sorted[k + 1] = v;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * kPopSortNT;
+            if (i >= N) break;
+            const int c = pp[u].w >= 0.0f ? cell_index<float>(pp[u].x, pp[u].y, pp[u].z, lo, inv, nb) : ncell;
+            const uint32_t sh = (uint32_t)(c & 1) << 4;
+            const uint32_t old = atomicAdd(&cw[c >> 1], 1u << sh);
+            slotn[i] = (int)(((uint32_t)c << 16) | ((old >> sh) & 0xffffu));
+        }
     }
+    __syncthreads();
+    // exclusive scan of the u16 counts in place (offsets <= N < 65536 fit the halves)
+    {
+        const int cpt = (nw + kPopSortNT - 1) / kPopSortNT, k0 = t * cpt;
+        uint32_t sum = 0;
+        for (int k = k0; k < k0 + cpt && k < nw; ++k) sum += (cw[k] & 0xffffu) + (cw[k] >> 16);
+        uint32_t incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[w] = (int)incl;
+        __syncthreads();
+        uint32_t run = incl - sum;
+        for (int i = 0; i < w; ++i) run += (uint32_t)wsum[i];
+        for (int k = k0; k < k0 + cpt && k < nw; ++k) {
+            const uint32_t v = cw[k], lo16 = run, hi16 = run + (v & 0xffffu);
+            run = hi16 + (v >> 16);
+            cw[k] = lo16 | (hi16 << 16);
+        }
+    }
+    __syncthreads();
+    auto off = [&](int c) -> int { return (int)((cw[c >> 1] >> ((c & 1) << 4)) & 0xffffu); };
+    auto put = [&](int k, int v) {
+        if (IDS_LDS)
+            ids[k] = (uint16_t)v;
+        else
+            aidn[k] = v;
+    };
+    auto get = [&](int k) -> int { return IDS_LDS ? (int)ids[k] : aidn[k]; };
+    for (int i0 = t; i0 < N; i0 += U * kPopSortNT) {
+        uint32_t uu[U];
+        int aa[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * kPopSortNT < N ? i0 + u * kPopSortNT : 0;
+            uu[u] = (uint32_t)slotn[i];
+            aa[u] = aido[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * kPopSortNT < N) put(off((int)(uu[u] >> 16)) + (int)(uu[u] & 0xffffu), aa[u]);
+    }
+    __syncthreads();
+    for (int c = t; c <= ncell; c += kPopSortNT) {  // deterministic order inside a cell
+        const int beg = off(c), end = off(c + 1);
+        for (int i = beg + 1; i < end; ++i) {
+            const int v = get(i);
+            int k = i - 1;
+            while (k >= beg && get(k) > v) {
+                put(k + 1, get(k));
+                --k;
+            }
+            put(k + 1, v);
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < N; i += kPopSortNT) {
+        const int a = get(i);
+        if (IDS_LDS) aidn[i] = a;
+        slotn[a] = i;
+    }
+    int* cg = A.cell + (size_t)s * kPopCells;
+    for (int c = t; c <= ncell + 1; c += kPopSortNT) cg[c] = off(c);
+    if (t == 0) A.par[s] = q;
 }
 
+// LDS bytes of pop_sort_kernel<IDS_LDS>
+__host__ __device__ inline size_t pop_sort_lds(bool ids_lds, int natom) {
+    return sizeof(uint32_t) * ((kPopCells + 1) / 2) + (ids_lds ? sizeof(uint16_t) * (size_t)natom : 0);
+}
+
+// logical block of the build kernels over the compacted flagged structures (plain
+// order: the working blocks are dealt over all XCDs); false for an idle block
+__device__ __forceinline__ bool pop_build_slot(const PopArgs& A, int* s, int* i) {
+    const int k = blockIdx.x / A.nbs;
+    if (k >= *A.nflag) return false;
+    *s = A.flist[k];
+    *i = (blockIdx.x % A.nbs) * kPopBS + threadIdx.x;
+    return *i < A.cm.natom;
+}
+
+// state and bonds of every slot of a flagged structure into its new slot order
+__global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
+    int s, i;
+    if (!pop_build_slot(A, &s, &i)) return;
+    const size_t base = (size_t)s * A.cm.ldn, k = base + i;
+    const int q = A.par[s], p = q ^ 1;
+    const PopBuf &O = A.buf[p], &B = A.buf[q];
+    const int a = B.aid[k];
+    const size_t o = base + O.slot[base + a];
+    const float4 x = O.pos[o];
+    B.pos[k] = x;
+    B.vel[k] = O.vel[o];
+    B.frc[k] = O.frc[o];
+    A.xb[k] = make_float4(x.x, x.y, x.z, 0.f);
+    // the atom's bonds (sorted adjacency of prepare()) with partners as slots
+    const Bonds& Bd = A.cm.bonds;
+    const int nsl = A.cm.nslice;
+    const int deg = Bd.deg[(size_t)s * A.cm.natom + a];
+    const uint32_t* g = Bd.ent + Bd.base[s] + Bd.soff[(size_t)s * (nsl + 1) + (a >> 6)] + (a & 63);
+    uint32_t* d = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
+    const int* sl = B.slot + base;
+    for (int e = 0; e < deg; ++e) {
+        const uint32_t v = g[(size_t)e * 64];
+        d[(size_t)e * 64] = (v & 0xffff0000u) | (uint32_t)sl[v & 0xffffu];
+    }
+    A.bdeg[k] = (uint16_t)deg;
+}
+
+// Verlet list of every bead slot of a flagged structure: the 27 cells around its cell,
+// each x-run of cells one contiguous slot range (visited in slot order)
 __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
-    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
-    if (s >= A.cm.nstruct) return;
-    if (!A.flag[s] || a >= A.cm.natom) return;
-    BigWs<float> W;
-    const NList<float, int> L = pop_list(A, s, &W);
-    const float4 p0 = W.pos[a];
-    A.xb4[(size_t)s * A.cm.ldn + a] = make_float4(p0.x, p0.y, p0.z, 0.f);
+    int s, i;
+    if (!pop_build_slot(A, &s, &i)) return;
+    const size_t base = (size_t)s * A.cm.ldn;
+    const float4* pos = A.buf[A.par[s]].pos + base;
+    const float4 p0 = pos[i];
+    const float* gp = A.gp + (size_t)s * 8;
+    const int* gn = A.gn + (size_t)s * 8;
+    const int* cell = A.cell + (size_t)s * kPopCells;
+    const int kcap = A.cm.kcap;
+    uint16_t* out = A.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * kcap * 64 + (i & 63);
     const float cut2 = A.P.cut_list * A.P.cut_list;
-    const int cap = L.kl + L.kg;
     int k = 0;
     if (p0.w >= 0.0f) {
-        walk27(cell_index<float>(p0.x, p0.y, p0.z, L.gp, L.gp + 3, L.gn), L.cell, L.sorted, L.gn,
+        walk27(cell_index<float>(p0.x, p0.y, p0.z, gp, gp + 3, gn), cell, (const uint16_t*)nullptr, gn,
                [&](int j, bool ok) {
-                   const float4 p = W.pos[j];
+                   const float4 p = pos[j];
                    const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
-                   const bool in = ok && j != a && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
-                   if (in && k < cap) L.gell[((size_t)(a >> 6) * L.kg + k) * 64 + (a & 63)] = (uint16_t)j;
+                   const bool in = ok && j != i && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
+                   if (in && k < kcap) out[(size_t)k * 64] = (uint16_t)j;
                    k += in ? 1 : 0;
                });
     }
-    L.nnb[a] = (uint16_t)(k <= cap ? k : kNnbWalk);
+    A.nnb[base + i] = (uint16_t)(k <= kcap ? k : kNnbWalk);
 }
 
-__global__ void __launch_bounds__(kPopBS) pop_forces_kernel(PopArgs A, float evf, float envf) {
-    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+// f32 force on slot i of structure s: the MD force path of atom_force specialised
+// for the population engine -- slot-space Verlet list and bonds, hardware rsq/rcp in
+// place of the IEEE sqrt/divide expansions, no calls (a call would put the kernel
+// arguments in scratch).  Neighbours and bond partners are loaded a batch at a time
+// so their gathers are in flight together; a masked tail keeps the batch branch-free.
+__device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, size_t base, const float4* pos,
+                                               uint32_t fl, float evf, float envf, float& fx, float& fy,
+                                               float& fz) {
+    constexpr int U = kPopPairBatch;
+    const int nsl = A.cm.nslice, amax = A.cm.natom - 1;
+    const uint16_t* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.cm.kcap * 64 + (i & 63);
+    const uint32_t* g = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
+    const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
+    const float4 p0 = pos[i];
+    const float xi = p0.x, yi = p0.y, zi = p0.z, ri = p0.w;
+    fx = fy = fz = 0.0f;
+    const float evfpi = evf * 0.318309886183790671537767526745f;
+    const int nn = A.nnb[base + i];
+    const int deg = A.bdeg[base + i];
+    auto pair = [&](const float4& p, bool on) {
+        const float dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
+        const float f = soft_pair_bf(dx * dx + dy * dy + dz * dz, ri + p.w, evfpi);
+        const float m = on ? f : 0.0f;
+        fx += m * dx;
+        fy += m * dy;
+        fz += m * dz;
+    };
+    auto bond = [&](const float4& p, float2 c, uint32_t e, bool on) {
+        const float dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
+        const float r2 = dx * dx + dy * dy + dz * dz;
+        const float rinv = __builtin_amdgcn_rsqf(fmaxf(r2, 1.0e-30f));
+        const float dr = r2 * rinv - c.x;
+        const bool active = (e & kLowerBit) ? (dr < 0.0f) : (dr > 0.0f);
+        const float m = (on && active && r2 > 0.0f) ? -2.0f * c.y * dr * rinv : 0.0f;
+        fx += m * dx;
+        fy += m * dy;
+        fz += m * dz;
+    };
+    if (ri >= 0.0f) {
+        if (nn == kNnbWalk) {
+            const float4 b = A.xb[base + i];
+            const float* gp = A.gp + (size_t)s * 8;
+            const int* gn = A.gn + (size_t)s * 8;
+            walk27(cell_index<float>(b.x, b.y, b.z, gp, gp + 3, gn), A.cell + (size_t)s * kPopCells,
+                   (const uint16_t*)nullptr, gn, [&](int j, bool ok) { pair(pos[j], ok && j != i); });
+        } else {
+            for (int k0 = 0; k0 < nn; k0 += U) {
+                int jt[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) jt[u] = min((int)gl[(size_t)(k0 + u) * 64], amax);
+                float4 pt[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) pt[u] = pos[jt[u]];
+#pragma unroll
+                for (int u = 0; u < U; ++u) pair(pt[u], k0 + u < nn);
+            }
+        }
+    }
+    for (int k0 = 0; k0 < deg; k0 += 4) {
+        uint32_t et[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) et[u] = g[(size_t)min(k0 + u, deg - 1) * 64];
+        float4 pt[4];
+        float2 ct[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            pt[u] = pos[et[u] & 0xffffu];
+            ct[u] = bt[(et[u] >> 16) & 0x7fffu];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bond(pt[u], ct[u], et[u], k0 + u < deg);
+    }
+    // envelopes (non-bead atoms carry -(radius + 1))
+    const float rad = ri >= 0.0f ? ri : -ri - 1.0f;
+    for (int e = 0; e < A.P.nenv; ++e) {
+        if (!(fl & (IGM_ATOM_ENV0 << e))) continue;
+        if (A.P.env_kind[e] == IGM_ENV_VOLUME) {
+            double en = 0.0;
+            volume_term<float, false>(xi, yi, zi, A.P.vmaps[A.P.vsmap ? A.P.vsmap[s] : 0], A.P.vvox, envf,
+                                      A.P.env_k[e], fx, fy, fz, en);
+            continue;
+        }
+        const float k = A.P.env_k[e];
+        const float sx = A.P.env_abc[e][0] * envf - rad, sy = A.P.env_abc[e][1] * envf - rad,
+                    sz = A.P.env_abc[e][2] * envf - rad;
+        const float ix = __builtin_amdgcn_rcpf(sx * sx), iy = __builtin_amdgcn_rcpf(sy * sy),
+                    iz = __builtin_amdgcn_rcpf(sz * sz);
+        const float k2 = xi * xi * ix + yi * yi * iy + zi * zi * iz;
+        const bool active = (k > 0.0f) ? (k2 > 1.0f) : (k2 < 1.0f && k2 > 0.0f);
+        if (!active) continue;
+        const float r2 = xi * xi + yi * yi + zi * zi;
+        const float rinv = __builtin_amdgcn_rsqf(r2), rsk = __builtin_amdgcn_rsqf(k2);
+        const float rn = r2 * rinv;
+        const float t = (1.0f - rsk) * rn;
+        const float ca = (1.0f - rsk) * rinv, cb = rn * rsk * __builtin_amdgcn_rcpf(k2);
+        const float ka = fabsf(k);
+        fx -= ka * t * (ca * xi + cb * xi * ix);
+        fy -= ka * t * (ca * yi + cb * yi * iy);
+        fz -= ka * t * (ca * zi + cb * zi * iz);
+    }
+    if (fl & IGM_ATOM_FIXED) fx = fy = fz = 0.0f;  // fix setforce 0 (lammps.py:222-223)
+}
+
+// forces of every slot (+ final_integrate and this block's kinetic-energy partial
+// when S.integrate; the run's setup evaluation otherwise)
+__global__ void __launch_bounds__(kPopBS) pop_force_kernel(PopArgs A, float evf, float envf, PopStep S) {
+    __shared__ double red[kPopBS / 64];
+    const int lb = pop_block(), s = lb / A.nbs, blk = lb % A.nbs, i = blk * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
-    if (a == 0 && A.flag[s]) {  // the structure's list was rebuilt this step
+    if (lb == 0 && threadIdx.x == 0) *A.nflag = 0;  // the build kernels of this step are done
+    if (i == 0 && A.flag[s]) {  // the structure's list was rebuilt this step
         A.flag[s] = 0;
         A.nrebuild[s] += 1;
     }
-    if (a >= A.cm.natom) return;
-    BigWs<float> W;
-    const NList<float, int> L = pop_list(A, s, &W);
-    const size_t i = (size_t)s * A.cm.ldn + a;
-    const uint32_t* adj = A.cm.bonds.ent + A.cm.bonds.base[s];
-    const int* soff = A.cm.bonds.soff + (size_t)s * (A.cm.nslice + 1);
-    const BondView B{adj + soff[a >> 6] + (a & 63), A.cm.bonds.types + A.cm.bonds.tbase[s], nullptr, nullptr,
-                     A.cm.bonds.deg[(size_t)s * A.cm.natom + a]};
-    const float4 b = A.xb4[i];
-    double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
-    float fx, fy, fz;
-    atom_force<float, false, int, kPopPairBatch>(s, a, W.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], W.pos, L, b.x, b.y, b.z, B, A.P, evf, envf, fx, fy,
-                                  fz, ep, eb, ee);
-    A.f4[i] = make_float4(fx, fy, fz, 0.f);
-}
-
-// final_integrate + this block's kinetic-energy partial
-__global__ void __launch_bounds__(kPopBS) pop_kick_kernel(PopArgs A, PopStep S) {
-    __shared__ double red[kPopBS / 64];
-    const int lb = pop_block(A), s = lb / A.nbs, blk = lb % A.nbs, a = blk * kPopBS + threadIdx.x;
-    if (s >= A.cm.nstruct) return;
+    const size_t base = (size_t)s * A.cm.ldn, k = base + i;
+    const PopBuf& B = A.buf[A.par[s]];
     double ke = 0.0;
-    if (a < A.cm.natom && !(A.cm.aflags[(size_t)s * A.cm.afs + a] & IGM_ATOM_FIXED)) {
-        const size_t i = (size_t)s * A.cm.ldn + a;
-        float4 v = A.v4[i];
-        const float4 f = A.f4[i];
-        kick_limit(v.x, v.y, v.z, f.x, f.y, f.z, S.dtf, S.vlim, S.vlimsq);
-        A.v4[i] = v;
-        ke = (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z);
+    if (i < A.cm.natom) {
+        float4 v = B.vel[k];
+        const uint32_t fl = __float_as_uint(v.w);
+        float fx, fy, fz;
+        pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz);
+        B.frc[k] = make_float4(fx, fy, fz, 0.f);
+        if (S.integrate && !(fl & IGM_ATOM_FIXED)) {
+            kick_limit(v.x, v.y, v.z, fx, fy, fz, S.dtf, S.vlim, S.vlimsq);
+            B.vel[k] = v;
+            ke = (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z);
+        }
     }
+    if (!S.integrate) return;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) ke += __shfl_xor(ke, off);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ke;
@@ -1196,39 +1424,45 @@ __global__ void __launch_bounds__(kPopBS) pop_kick_kernel(PopArgs A, PopStep S) 
     }
 }
 
-// end of a run: the last step's rescale, then (optionally) the outputs
+// end of a run: the last step's rescale, then (optionally) the outputs in atom order
 __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S, float* xyz, float* vel,
                                                             float* forces_out) {
     __shared__ float fac;
-    const int lb = pop_block(A), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
+    const int lb = pop_block(), s = lb / A.nbs, i = (lb % A.nbs) * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
     const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
-    if (a >= A.cm.natom) return;
-    const size_t i = (size_t)s * A.cm.ldn + a;
-    float4 v = A.v4[i];
+    if (i >= A.cm.natom) return;
+    const PopBuf& B = A.buf[A.par[s]];
+    const size_t k = (size_t)s * A.cm.ldn + i;
+    float4 v = B.vel[k];
     v.x *= factor;
     v.y *= factor;
     v.z *= factor;
-    A.v4[i] = v;
+    B.vel[k] = v;
     if (!xyz) return;  // more runs follow
-    BigWs<float> W;
-    pop_list(A, s, &W);
-    const float4 p = W.pos[a];
-    float* xo = xyz + ((size_t)s * A.cm.natom + a) * 3;
-    xo[0] = p.x;
-    xo[1] = p.y;
-    xo[2] = p.z;
-    float* vo = vel + ((size_t)s * A.cm.natom + a) * 3;
-    vo[0] = v.x;
-    vo[1] = v.y;
-    vo[2] = v.z;
+    const size_t a = (size_t)s * A.cm.natom + B.aid[k];
+    const float4 p = B.pos[k];
+    xyz[a * 3] = p.x;
+    xyz[a * 3 + 1] = p.y;
+    xyz[a * 3 + 2] = p.z;
+    vel[a * 3] = v.x;
+    vel[a * 3 + 1] = v.y;
+    vel[a * 3 + 2] = v.z;
     if (forces_out) {
-        const float4 f = A.f4[i];
-        float* fo = forces_out + ((size_t)s * A.cm.natom + a) * 3;
-        fo[0] = f.x;
-        fo[1] = f.y;
-        fo[2] = f.z;
+        const float4 f = B.frc[k];
+        forces_out[a * 3] = f.x;
+        forces_out[a * 3 + 1] = f.y;
+        forces_out[a * 3 + 2] = f.z;
     }
+}
+
+__global__ void deg_max_kernel(const int* deg, size_t n, int* out) {
+    int m = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        m = max(m, deg[i]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
 
 // 'velocity nonfixed create T seed' (dist uniform, loop all, mom yes) for every
@@ -2185,42 +2419,105 @@ int resident_grid(igm_ctx* c, KernelT kernel, int nt, size_t lds, int nstruct, i
 }
 
 
-// The population engine (HBM path): per step  kick+drift+check | list builds | forces |
-// kick + temperature partials, over every atom of every structure.
+// the structures [s0, s0 + ns) of a population engine as an engine of their own
+// (per-structure pointers offset; flag counter g)
+PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
+    PopArgs V = Q;
+    const size_t ldn = Q.cm.ldn, nsl = Q.cm.nslice, o = (size_t)s0 * ldn;
+    V.cm.nstruct = ns;
+    V.cm.aflags = Q.cm.aflags + (size_t)s0 * Q.cm.afs;
+    V.cm.bonds.base = Q.cm.bonds.base + s0;
+    V.cm.bonds.soff = Q.cm.bonds.soff + (size_t)s0 * (nsl + 1);
+    V.cm.bonds.deg = Q.cm.bonds.deg + (size_t)s0 * Q.cm.natom;
+    V.cm.bonds.tbase = Q.cm.bonds.tbase + s0;
+    V.cm.bonds.ntype = Q.cm.bonds.ntype + s0;
+    if (V.P.vsmap) V.P.vsmap = Q.P.vsmap + s0;
+    for (int b = 0; b < 2; ++b)
+        V.buf[b] = PopBuf{Q.buf[b].pos + o, Q.buf[b].vel + o, Q.buf[b].frc + o, Q.buf[b].aid + o, Q.buf[b].slot + o};
+    V.par = Q.par + s0;
+    V.xb = Q.xb + o;
+    V.nl = Q.nl + (size_t)s0 * nsl * Q.cm.kcap * 64;
+    V.nnb = Q.nnb + o;
+    V.cell = Q.cell + (size_t)s0 * kPopCells;
+    V.gp = Q.gp + (size_t)s0 * 8;
+    V.gn = Q.gn + (size_t)s0 * 8;
+    V.bent = Q.bent + (size_t)s0 * nsl * Q.bdmax * 64;
+    V.bdeg = Q.bdeg + o;
+    V.flag = Q.flag + s0;
+    V.flist = Q.flist + s0;
+    V.nflag = Q.nflag + g;
+    V.nrebuild = Q.nrebuild + s0;
+    V.kep = Q.kep + (size_t)s0 * Q.nbs;
+    V.bbp = Q.bbp + (size_t)s0 * Q.nbs * 6;
+    V.dofs = Q.dofs + s0;
+    return V;
+}
+
+// The population engine (HBM path): per step  integrate | [sort | permute | fill of the
+// flagged structures] | forces + final kick, over every slot of every structure.
 int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
-    const int S = pr.cm.nstruct, N = pr.cm.natom, ldn = pr.cm.ldn;
+    const int S = pr.cm.nstruct, N = pr.cm.natom, ldn = pr.cm.ldn, nsl = pr.cm.nslice;
     PopArgs Q;
     memset(&Q, 0, sizeof(Q));
     Q.cm = pr.cm;
     Q.P = pr.P;
     Q.nbs = (N + kPopBS - 1) / kPopBS;
-    NList<float, int> L;
-    BigWs<float> W;
-    Q.ws_stride = carve_ws<float>(nullptr, N, ldn, pr.cm.kcap, kCellCapBig, true, false, &L, &W);
-    void *ws, *pv, *pf, *pb, *pgp, *pgn, *pfl, *pke, *pbb, *pnc;
-    IGM_TRY(workspace(c, "pop_ws", Q.ws_stride * (size_t)S, &ws));
-    IGM_TRY(workspace(c, "pop_v", sizeof(float4) * (size_t)S * ldn, &pv));
-    IGM_TRY(workspace(c, "pop_f", sizeof(float4) * (size_t)S * ldn, &pf));
-    IGM_TRY(workspace(c, "pop_xb", sizeof(float4) * (size_t)S * ldn, &pb));
+    const size_t SL = (size_t)S * ldn;
+    // the largest bond degree sizes the slot-ordered bond ELL
+    void* pdm;
+    IGM_TRY(workspace(c, "pop_dmax", sizeof(int), &pdm));
+    IGM_HIP_CHECK(c, hipMemsetAsync(pdm, 0, sizeof(int), c->stream));
+    hipLaunchKernelGGL(deg_max_kernel, dim3(1024), dim3(256), 0, c->stream, pr.cm.bonds.deg, (size_t)S * N, (int*)pdm);
+    int dmax = 0;
+    IGM_HIP_CHECK(c, hipMemcpyAsync(&dmax, pdm, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    if (dmax > 0xFFFF) return fail(c, IGM_E_UNSUPPORTED, "an atom has %d bonds", dmax);
+    Q.bdmax = dmax > 0 ? dmax : 1;
+    for (int b = 0; b < 2; ++b) {
+        char nm[5][16];
+        const char* what[5] = {"pos", "vel", "frc", "aid", "slot"};
+        void* p[5];
+        const size_t sz[5] = {sizeof(float4), sizeof(float4), sizeof(float4), sizeof(int), sizeof(int)};
+        for (int k = 0; k < 5; ++k) {
+            snprintf(nm[k], sizeof(nm[k]), "pop_%s%d", what[k], b);
+            IGM_TRY(workspace(c, nm[k], sz[k] * SL, &p[k]));
+        }
+        Q.buf[b] = PopBuf{(float4*)p[0], (float4*)p[1], (float4*)p[2], (int*)p[3], (int*)p[4]};
+    }
+    void *ppar, *pxb, *pnl, *pnnb, *pcell, *pgp, *pgn, *pbent, *pbdeg, *pfl, *pfli, *pnf, *pke, *pbb;
+    IGM_TRY(workspace(c, "pop_par", sizeof(int) * S, &ppar));
+    IGM_TRY(workspace(c, "pop_xb", sizeof(float4) * SL, &pxb));
+    // + slack: the batched force loop reads up to kPopPairBatch - 1 slots past a list
+    IGM_TRY(workspace(c, "pop_nl", sizeof(uint16_t) * (SL * pr.cm.kcap + 64 * kPopPairBatch), &pnl));
+    IGM_TRY(workspace(c, "pop_nnb", sizeof(uint16_t) * SL, &pnnb));
+    IGM_TRY(workspace(c, "pop_cell", sizeof(int) * (size_t)S * kPopCells, &pcell));
     IGM_TRY(workspace(c, "pop_gp", sizeof(float) * 8 * (size_t)S, &pgp));
     IGM_TRY(workspace(c, "pop_gn", sizeof(int) * 8 * (size_t)S, &pgn));
+    IGM_TRY(workspace(c, "pop_bent", sizeof(uint32_t) * SL * Q.bdmax, &pbent));
+    IGM_TRY(workspace(c, "pop_bdeg", sizeof(uint16_t) * SL, &pbdeg));
     IGM_TRY(workspace(c, "pop_flag", sizeof(int) * (size_t)S, &pfl));
+    IGM_TRY(workspace(c, "pop_flist", sizeof(int) * (size_t)S, &pfli));
+    IGM_TRY(workspace(c, "pop_nflag", sizeof(int) * 64, &pnf));
     IGM_TRY(workspace(c, "pop_ke", sizeof(double) * (size_t)S * Q.nbs, &pke));
     IGM_TRY(workspace(c, "pop_bb", sizeof(float) * 6 * (size_t)S * Q.nbs, &pbb));
-    IGM_TRY(workspace(c, "pop_nc", sizeof(int) * (size_t)S, &pnc));
     void* pnr = A.nrebuild;
     if (!pnr) IGM_TRY(workspace(c, "pop_nreb", sizeof(int) * (size_t)S, &pnr));
-    Q.ws = (unsigned char*)ws;
-    Q.v4 = (float4*)pv;
-    Q.f4 = (float4*)pf;
-    Q.xb4 = (float4*)pb;
+    Q.par = (int*)ppar;
+    Q.xb = (float4*)pxb;
+    Q.nl = (uint16_t*)pnl;
+    Q.nnb = (uint16_t*)pnnb;
+    Q.cell = (int*)pcell;
     Q.gp = (float*)pgp;
     Q.gn = (int*)pgn;
+    Q.bent = (uint32_t*)pbent;
+    Q.bdeg = (uint16_t*)pbdeg;
     Q.flag = (int*)pfl;
+    Q.flist = (int*)pfli;
+    Q.nflag = (int*)pnf;
     Q.kep = (double*)pke;
     Q.bbp = (float*)pbb;
-    Q.ncell = (int*)pnc;
     Q.nrebuild = (int*)pnr;
+    (void)nsl;
     // dof of group nonfixed, per structure (atom flags may differ between structures)
     {
         const size_t nfl = pr.cm.afs ? (size_t)S * N : (size_t)N;
@@ -2241,18 +2538,51 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
         Q.dofs = (const double*)pdof;
     }
-    const dim3 grid((S * Q.nbs + 7) & ~7), blk(kPopBS);  // padded for pop_block
+    // the sort keeps its ids in LDS when they fit beside the cell counts (200 kb: 29 839 atoms)
+    const bool ids_lds = pop_sort_lds(true, N) <= kLdsBytes;
+    const size_t sort_lds = pop_sort_lds(ids_lds, N);
+    auto sort_kern = ids_lds ? pop_sort_kernel<true> : pop_sort_kernel<false>;
+    IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)sort_kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)sort_lds));
+    // Structure groups on auxiliary streams: while one group waits in its latency-bound
+    // sort, the others' force and integrate launches fill the CUs (measured on config C:
+    // 2 groups 11 % faster than 1, 4 and 8 slower).  Tuning knobs: IGM_POP_GROUPS groups,
+    // IGM_POP_CONC of them in flight together, IGM_POP_CHUNK steps per group before the
+    // next ones run (0: every group advances in lock step).
+    auto knob = [](const char* name, int dflt) {
+        const char* e = getenv(name);
+        return e ? atoi(e) : dflt;
+    };
+    int ng = knob("IGM_POP_GROUPS", 2), nc = knob("IGM_POP_CONC", 0), chunk = knob("IGM_POP_CHUNK", 0);
+    ng = ng < 1 ? 1 : (ng > S ? S : (ng > 64 ? 64 : ng));
+    nc = nc < 1 || nc > ng ? ng : nc;
+    if (chunk <= 0) nc = ng;
+    IGM_TRY(aux_streams(c, ng));
+    std::vector<PopArgs> V(ng);
+    std::vector<int> g0(ng + 1);
+    for (int g = 0; g <= ng; ++g) g0[g] = (int)((int64_t)S * g / ng);
+    for (int g = 0; g < ng; ++g) V[g] = pop_view(Q, g0[g], g0[g + 1] - g0[g], g);
+    auto grid_of = [&](int g) { return dim3(((g0[g + 1] - g0[g]) * Q.nbs + 7) & ~7); };  // padded for pop_block
+    auto strm = [&](int g) { return c->aux[g % nc]; };
+    const dim3 blk(kPopBS);
+    const size_t n3 = (size_t)N * 3;
     Timed tm(c, "anneal");
-    hipLaunchKernelGGL(pop_load_kernel, grid, blk, 0, c->stream, Q, (const float*)A.xyz);
-    if (A.nseg == 0) {  // no runs (CG only): velocities 0, positions unchanged
-        PopStep st;
-        memset(&st, 0, sizeof(st));
-        hipLaunchKernelGGL(pop_finish_kernel, grid, blk, 0, c->stream, Q, st, A.xyz, A.vel, A.forces_out);
+    IGM_TRY(aux_fork(c, nc));
+    for (int g = 0; g < ng; ++g) {
+        hipLaunchKernelGGL(pop_load_kernel, grid_of(g), blk, 0, strm(g), V[g], (const float*)A.xyz + g0[g] * n3);
+        if (A.nseg == 0) {  // no runs (CG only): velocities 0, positions unchanged
+            PopStep st;
+            memset(&st, 0, sizeof(st));
+            hipLaunchKernelGGL(pop_finish_kernel, grid_of(g), blk, 0, strm(g), V[g], st, A.xyz + g0[g] * n3,
+                               A.vel + g0[g] * n3, A.forces_out ? A.forces_out + g0[g] * n3 : nullptr);
+        }
     }
     for (int seg = 0; seg < A.nseg; ++seg) {
-        const float* vsrc = A.mode == 1 ? A.vel : A.vinit + (size_t)seg * N * 3;
-        const size_t sstride = A.mode == 1 ? (size_t)N * 3 : (size_t)A.nseg * N * 3;
-        hipLaunchKernelGGL(pop_setvel_kernel, grid, blk, 0, c->stream, Q, vsrc, sstride);
+        const float* vsrc = A.mode == 1 ? A.vel : A.vinit + (size_t)seg * n3;
+        const size_t sstride = A.mode == 1 ? n3 : (size_t)A.nseg * n3;
+        for (int g = 0; g < ng; ++g)
+            hipLaunchKernelGGL(pop_setvel_kernel, grid_of(g), blk, 0, strm(g), V[g], vsrc + g0[g] * sstride,
+                               sstride);
         PopStep st;
         memset(&st, 0, sizeof(st));
         st.dtv = A.dt;
@@ -2266,29 +2596,37 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         st.window = A.t_window;
         st.fraction = A.t_fraction;
         const float evf = A.seg_evf[seg], envf = A.seg_envf[seg];
-        for (int step = 0; step <= st.nsteps; ++step) {
-            st.integrate = step > 0;
-            st.rescale = step > 1;
-            st.prev = step - 1;
-            hipLaunchKernelGGL(pop_kick_drift_kernel, grid, blk, 0, c->stream, Q, st);
-            // list builds of the flagged structures (every launch exits at once for the others)
-            hipLaunchKernelGGL(pop_grid_kernel, dim3(S), dim3(256), 0, c->stream, Q);
-            hipLaunchKernelGGL(pop_count_kernel, grid, blk, 0, c->stream, Q);
-            hipLaunchKernelGGL(pop_scan_kernel, dim3(S), dim3(1024), 0, c->stream, Q);
-            hipLaunchKernelGGL(pop_scatter_kernel, grid, blk, 0, c->stream, Q);
-            hipLaunchKernelGGL(pop_cellsort_kernel, dim3(S * kPopCellBlocks), dim3(256), 0, c->stream, Q);
-            hipLaunchKernelGGL(pop_fill_kernel, grid, blk, 0, c->stream, Q);
-            hipLaunchKernelGGL(pop_forces_kernel, grid, blk, 0, c->stream, Q, evf, envf);
-            if (step > 0) hipLaunchKernelGGL(pop_kick_kernel, grid, blk, 0, c->stream, Q, st);
+        const int span = chunk > 0 ? chunk : st.nsteps + 1;
+        for (int c0 = 0; c0 <= st.nsteps; c0 += span) {
+            const int c1 = c0 + span - 1 < st.nsteps ? c0 + span - 1 : st.nsteps;
+            for (int w0 = 0; w0 < ng; w0 += nc) {  // groups w0 .. w0 + nc - 1 run steps c0..c1 together
+                for (int step = c0; step <= c1; ++step) {
+                    st.integrate = step > 0;
+                    st.rescale = step > 1;
+                    st.prev = step - 1;
+                    for (int g = w0; g < w0 + nc && g < ng; ++g) {
+                        const int ns = g0[g + 1] - g0[g];
+                        hipStream_t sg = strm(g);
+                        hipLaunchKernelGGL(pop_integrate_kernel, grid_of(g), blk, 0, sg, V[g], st);
+                        hipLaunchKernelGGL(sort_kern, dim3(ns), dim3(kPopSortNT), sort_lds, sg, V[g]);
+                        hipLaunchKernelGGL(pop_permute_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                        hipLaunchKernelGGL(pop_fill_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                        hipLaunchKernelGGL(pop_force_kernel, grid_of(g), blk, 0, sg, V[g], evf, envf, st);
+                    }
+                }
+            }
         }
         IGM_HIP_CHECK(c, hipGetLastError());
         st.rescale = st.nsteps > 0;
         st.prev = st.nsteps;
         const bool last = seg + 1 == A.nseg;
-        hipLaunchKernelGGL(pop_finish_kernel, grid, blk, 0, c->stream, Q, st, last ? A.xyz : nullptr,
-                           last ? A.vel : nullptr, last ? A.forces_out : nullptr);
+        for (int g = 0; g < ng; ++g)
+            hipLaunchKernelGGL(pop_finish_kernel, grid_of(g), blk, 0, strm(g), V[g], st,
+                               last ? A.xyz + g0[g] * n3 : nullptr, last ? A.vel + g0[g] * n3 : nullptr,
+                               last && A.forces_out ? A.forces_out + g0[g] * n3 : nullptr);
     }
     IGM_HIP_CHECK(c, hipGetLastError());
+    IGM_TRY(aux_join(c, nc));
     return IGM_OK;
 }
 

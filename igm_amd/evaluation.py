@@ -7,7 +7,8 @@ HicEvaluationStep).
                       |x_i - x_j| <= fl32(contact_range * fl32(r_i + r_j)).
   contact_map      -- reduce()'s output matrix (:108-113): counts / nstruct at
                       contactRange = contact_range * (1 + EPS), copies summed
-                      (sumCopies) and clipped to [0, 1].
+                      (sumCopies) on the device (igm_contact_map_haploid: no
+                      (nbead, nbead) matrix on the host) and clipped to [0, 1].
   hic_evaluation   -- reduce()'s score (:145-179): over the input pairs i != j with
                       p >= sigma that the output matrix stores (non-zero), the mean
                       absolute relative difference, plus the averages stats.txt holds.
@@ -41,8 +42,29 @@ def contact_counts(xyz, radii, contact_range, ctx=None, device=0):
     return out
 
 
+def haploid_counts(xyz, radii, contact_range, copy_ptr, copy_idx, ctx=None, device=0):
+    """The contact counts with the copies summed on the device (igm_contact_map_haploid):
+    (nhap, nhap) int32, entry (a, b) = sum of counts[a_k, b_l] over the copies -- no
+    (nbead, nbead) intermediate on the host."""
+    c = ctx or _lib.context(device)
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    radii = np.ascontiguousarray(radii, np.float32)
+    copy_ptr = np.ascontiguousarray(copy_ptr, np.int32)
+    copy_idx = np.ascontiguousarray(copy_idx, np.int32)
+    if xyz.ndim != 3 or xyz.shape[2] != 3 or radii.shape != (xyz.shape[0],):
+        raise ValueError('xyz must be (nbead, nstruct, 3) and radii (nbead,)')
+    nbead, S = xyz.shape[0], xyz.shape[1]
+    nhap = len(copy_ptr) - 1
+    out = np.empty((nhap, nhap), np.int32)
+    rc = c.lib.igm_contact_map_haploid(c.h, 0, xyz.ctypes.data, nbead, S, radii.ctypes.data, float(contact_range),
+                                       copy_ptr.ctypes.data, copy_idx.ctypes.data, nhap, out.ctypes.data)
+    c.check(rc, 'igm_contact_map_haploid')
+    return out
+
+
 def sum_copies(full, copy_ptr, copy_idx):
-    """(nbead, nbead) -> (nhap, nhap): entry (a, b) sums full over the copies of a and b."""
+    """(nbead, nbead) -> (nhap, nhap): entry (a, b) sums full over the copies of a and b
+    (host restatement of sumCopies; small inputs and tests only)."""
     nhap = len(copy_ptr) - 1
     hap_of = np.empty(len(copy_idx), np.int64)
     for a in range(nhap):
@@ -53,10 +75,11 @@ def sum_copies(full, copy_ptr, copy_idx):
 
 
 def contact_map(xyz, radii, contact_range, copy_ptr, copy_idx, ctx=None, device=0):
-    """reduce()'s out_matrix: haploid contact frequencies clipped to [0, 1]."""
-    counts = contact_counts(xyz, radii, contact_range * (1 + EPS), ctx=ctx, device=device)
-    full = counts / np.float64(xyz.shape[1])
-    return np.clip(sum_copies(full, copy_ptr, copy_idx), 0, 1)
+    """reduce()'s out_matrix: haploid contact frequencies clipped to [0, 1].  The copies
+    are summed as integers on the device and divided by nstruct once (the reference
+    divides first, then sums float64 copies: equal up to the last bit of the sum)."""
+    counts = haploid_counts(xyz, radii, contact_range * (1 + EPS), copy_ptr, copy_idx, ctx=ctx, device=device)
+    return np.clip(counts / np.float64(np.asarray(xyz).shape[1]), 0, 1)
 
 
 def hic_evaluation(input_matrix, output_matrix, sigma):

@@ -19,7 +19,8 @@ def optimize(model, cfg, ctx=None):
     lm = M.from_igm_model(model)
     prm = M.params_from_cfg(cfg, lm.envelopes, evfactor=lm.evfactor)
     opt = cfg['optimization']['optimizer_options']
-    step_no = cfg.get('runtime', {}).get('step_no', 0) if hasattr(cfg, 'get') else 0
+    # cfg.get('runtime/step_no', 1) as lammps.py:435 reads it (Config keypath get)
+    step_no = cfg.get('runtime', {}).get('step_no', 1) if hasattr(cfg, 'get') else 1
     seeds = M.lammps_seeds(opt.get('seed', 6535), [lm.id], step_no)
     t0 = time.time()
     x, info = mstep.run(prm, lm.xyz[None], lm.radii, lm.flags, lm.bonds, None, None, seeds, ctx=ctx)

@@ -90,6 +90,11 @@ class AMIteration(object):
         xyz_local = np.ascontiguousarray(xyz_local, np.float32)
         self.S_local, self.natom = xyz_local.shape[0], xyz_local.shape[1]
         self.nbead = int(atoms.nbead)
+        if world > 1:  # gather_population all-gathers equal blocks: every rank must hold as many structures
+            counts = self._all_counts(self.S_local)
+            if len(set(counts)) != 1:
+                raise ValueError('structure shards must be equal (got %s per rank): pad the population to a '
+                                 'multiple of the world size' % counts)
         self.S_total = self.S_local * world
         self.xyz = T(xyz_local)                                  # (S_local, natom, 3) M-step layout
         self.radii = T(atoms.radii)
@@ -120,6 +125,14 @@ class AMIteration(object):
         self.pop_bm = torch.empty((self.nbead, self.S_total, 3), dtype=torch.float32, device=self.dev)
 
     # ------------------------------------------------------------------ helpers
+    def _all_counts(self, n):
+        import torch.distributed as dist
+        t = self.torch.tensor([int(n)], dtype=self.torch.int64,
+                              device=self.dev if dist.get_backend(self.group) == 'nccl' else 'cpu')
+        parts = [self.torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t, group=self.group)
+        return [int(p.item()) for p in parts]
+
     def _call(self, fn, *args):
         c = self.ctx
         c.set_stream(self.torch.cuda.current_stream(self.dev).cuda_stream)

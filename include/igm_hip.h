@@ -176,6 +176,16 @@ int igm_contact_map(igm_ctx* ctx, uint32_t flags,
                     const float* xyz, int32_t nbead, int32_t nstruct,
                     const float* radii, double contact_range, int32_t* counts);
 
+/* The same counts with the copies summed on the device (Contactmatrix.sumCopies,
+ * HicEvaluationStep.py:111-112): counts (nhap, nhap) int32 = sum over the copy pairs
+ * (a_k, b_l) of the diploid counts -- reduce()'s matrix before the division by nstruct,
+ * without the (nbead, nbead) intermediate (3.6 GB at 200 kb).  copy_ptr / copy_idx
+ * (host pointers, CSR of index.copy_index) must cover every bead exactly once. */
+int igm_contact_map_haploid(igm_ctx* ctx, uint32_t flags,
+                            const float* xyz, int32_t nbead, int32_t nstruct,
+                            const float* radii, double contact_range,
+                            const int32_t* copy_ptr, const int32_t* copy_idx, int32_t nhap, int32_t* counts);
+
 /* SPRITE: SpriteAssignmentStep.task (igm/steps/SpriteAssignmentStep.py:105-160):
  * compute_gyration_radius (igm/cython_compiled/sprite.pyx:104-283, get_rg2s_cpp
  * cpp_sprite_assignment.cpp:49-143) for every (cluster, structure), then keep_best.

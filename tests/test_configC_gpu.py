@@ -1,0 +1,105 @@
+"""The metric's workload (BASELINE.json configs[2], SURVEY 8(d) config C: 200 kb hg38
+male diploid, 29 838 beads, 1000 structures, synthetic .hcs at sigma 0.01) through the
+C ABI on the MI355X:
+
+  * the Hi-C A-step (ActivationDistanceStep.get_actdist, igm/steps/
+    ActivationDistanceStep.py:336-485) on the WHOLE 1.3 M-pair list: per-pair row
+    counts and the CSR row layout checked for every pair, and a seeded sample of
+    20 000 pairs bit-exact against the C oracle (rows, o, pnow, ad, p);
+  * the population engine (the HBM-resident M-step for structures past one CU's LDS)
+    running the whole demo protocol shape (4 stages + relax + CG, step counts scaled)
+    on 200 kb structures with frustrated Hi-C-like restraints, against the fp64
+    oracle (population statistics) and bitwise against its own rerun.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import oracle
+import mstep_stats as MS
+from igm_amd import model as M
+from igm_amd import synthetic as syn
+from igm_amd._lib import pair_dtype
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def popC():
+    pop = syn.population_200kb(1000)
+    xyz = np.ascontiguousarray(pop['xyz'].transpose(1, 0, 2))  # (nbead, S, 3), the .hss layout
+    i, j, p = syn.hic_pairs_200kb(0.01)
+    return pop, xyz, i, j, p
+
+
+def test_gpu_configC_actdist_every_pair(popC):
+    from igm_amd import astep
+    pop, xyz, i, j, p = popC
+    assert xyz.shape == (29838, 1000, 3) and len(i) > 1_290_000
+    rng = np.random.default_rng(2024)
+    pairs = np.zeros(len(i), pair_dtype)
+    pairs['i'], pairs['j'], pairs['pwish'] = i, j, p.astype(np.float64)
+    pairs['plast'] = np.where(rng.uniform(size=len(i)) < 0.5, rng.uniform(0, 0.6, len(i)), 0.0)
+    cp, ci, chrom = pop['copy_ptr'], pop['copy_idx'], pop['chrom']
+    rows, res = astep.compute_actdist(xyz, pop['radii'], cp, ci, chrom, pairs, 2.0, 1, return_per_pair=True)
+    # every pair: rows only when p > 0, then one per copy combination (zip for intra, all
+    # copy pairs for inter), in CSR pair order
+    nc = np.diff(cp)
+    intra = chrom[i] == chrom[j]  # the reference indexes index.chrom with the haploid ids (py:398-400)
+    ncomb = np.where(intra, np.minimum(nc[i], nc[j]), nc[i] * nc[j])
+    want = np.where(res['p'] > 0, ncomb, 0)
+    assert np.array_equal(res['nrows'], want.astype(np.int32))
+    assert len(rows) == int(want.sum())
+    first = np.concatenate([[0], np.cumsum(want)[:-1]])
+    has = want > 0
+    assert np.array_equal(rows['row'][first[has]], ci[cp[i[has]]])  # first combination: copy 0 x copy 0
+    assert np.array_equal(rows['col'][first[has]], ci[cp[j[has]]])
+    # ('%.4f' % p can print a p < 5e-5 as 0.0000)
+    assert np.all(rows['dist'] > 0) and np.all((rows['prob'] >= 0) & (rows['prob'] <= 1))
+    # a seeded 20 000-pair sample bit for bit against the oracle
+    sub = np.sort(rng.choice(len(i), 20000, replace=False))
+    orows, ores = oracle.actdist(xyz, pop['radii'], cp, ci, chrom, pairs[sub], 2.0, 1, nthreads=16)
+    for k in ('nrows', 'o', 'pnow', 'ad', 'p'):
+        a, b = res[k][sub], ores[k]
+        if k in ('ad', 'p'):
+            a, b = a[ores['nrows'] > 0], b[ores['nrows'] > 0]
+        assert np.array_equal(a, b), k
+    mine = np.concatenate([rows[first[q]:first[q] + want[q]] for q in sub if want[q] > 0])
+    assert mine.tobytes() == orows.tobytes()
+
+
+# ------------------------------------------------------------------ 200 kb protocol
+def _model200(n, nlocal=15000, nlong=1500, seed=31):
+    pop = syn.population_200kb(n, first_sid=500)
+    atoms = M.Atoms(pop['radii'])
+    poly = M.polymer_bonds(pop['chrom'], pop['copy'], pop['radii'], 2.0, 1.0)
+    x = np.zeros((n, atoms.n, 3), np.float32)
+    x[:, :atoms.nbead] = pop['xyz']
+    per = [MS.random_contacts(atoms.radii, atoms.nbead, nlocal, nlong, seed + s) for s in range(n)]
+    ptr, sb = M.concat_bonds(per)
+    return atoms, poly, ptr, sb, x
+
+
+def test_gpu_200kb_protocol_matches_oracle_and_reruns_bitwise():
+    from igm_amd import mstep
+    n = 8
+    atoms, poly, ptr, sb, x = _model200(n)
+    proto = MS.scaled_protocol(syn.DEMO_PROTOCOL, 0.02)  # 4 stages + relax + CG, 940 MD steps
+    prm = M.params_from_cfg({'optimization': {'optimizer_options': proto}}, [((5500.0,) * 3, 1.0)])
+    prm.skin = 0.55 * float(atoms.radii.max())  # the same Verlet skin on both sides
+    seeds = M.lammps_seeds(6535, np.arange(500, 500 + n), 3)
+    xg, ig = mstep.run(prm, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
+    xg2, ig2 = mstep.run(prm, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
+    assert np.array_equal(xg, xg2) and ig.tobytes() == ig2.tobytes()  # bitwise reproducible
+    assert np.all(np.isfinite(xg)) and np.all(ig['final_energy'] < ig['einitial'])
+    xo, io, _ = oracle.mstep_run(prm, x.copy(), atoms.radii, atoms.flags, poly, ptr, sb, seeds, nthreads=16)
+    sg = MS.population_stats(ig, xg, poly, ptr, sb, atoms.nbead)
+    so = MS.population_stats(io, xo, poly, ptr, sb, atoms.nbead)
+    # 8 chaotic trajectories per side: the medians of the per-structure energies per bead
+    # and violation fractions agree within 20 % (the 2x K / 2x evf perturbations of
+    # tests/test_mstep_stats.py move them by 25-140 %)
+    for k in ('pair', 'bond', 'total', 'viol_frac'):
+        a, b = np.median(sg[k]), np.median(so[k])
+        assert abs(a - b) <= 0.2 * max(abs(a), abs(b)) + 1e-9, (k, a, b)
+    assert np.all(ig['temp'] < 1.0) and np.all(io['temp'] < 1.0)

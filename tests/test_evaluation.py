@@ -108,3 +108,26 @@ def test_gpu_contact_counts_near_ties():
     ref = OA.contact_counts(crd, r, 2.0)
     assert got.tobytes() == ref.tobytes()
     assert 0 < ref[0, 1:].min() and ref[0, 1:].max() < S  # genuinely split decisions
+
+
+@pytest.mark.gpu
+def test_gpu_haploid_counts_equal_summed_copies(pop):
+    """igm_contact_map_haploid (copies summed on the device) equals the diploid counts
+    summed over copy pairs on the host, exactly (integer sums), on the demo population;
+    reduce()'s matrix then follows by one division."""
+    crd, r = pop['coordinates'], pop['radii']
+    cp, ci = pop['copy_ptr'], pop['copy_idx']
+    full = EV.contact_counts(crd, r, 2.0 * (1 + EV.EPS))
+    want = EV.sum_copies(full.astype(np.float64), cp, ci)
+    got = EV.haploid_counts(crd, r, 2.0 * (1 + EV.EPS), cp, ci)
+    assert np.array_equal(got.astype(np.float64), want)
+    m = EV.contact_map(crd, r, 2.0, cp, ci)
+    ref = np.clip(EV.sum_copies(full / np.float64(crd.shape[1]), cp, ci), 0, 1)
+    assert np.allclose(m, ref, rtol=1e-14, atol=0)
+
+
+@pytest.mark.gpu
+def test_gpu_haploid_counts_rejects_bad_copy_index(pop):
+    crd, r = pop['coordinates'][:4, :3], pop['radii'][:4]
+    with pytest.raises(RuntimeError):
+        EV.haploid_counts(crd, r, 2.0, np.array([0, 2, 3]), np.array([0, 1, 1]))  # bead 1 twice, 2 and 3 missing
