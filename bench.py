@@ -179,7 +179,7 @@ def bench_config_c(args, dev, ctx_threads):
     import torch
     from igm_amd.pipeline import AMIteration
     ca = argparse.Namespace(**vars(args))
-    ca.config, ca.nstruct, ca.sigma, ca.protocol_scale = 'C', 125, 0.01, 1.0
+    ca.config, ca.nstruct, ca.sigma = 'C', 125, 0.01  # protocol_scale: 1.0 for the metric
     inp = build_inputs(ca, 0)
     pop = inp['pop']
     it = AMIteration(dev, inp['xyz'], inp['atoms'], inp['chrom'], pop['copy_ptr'], pop['copy_idx'], inp['pairs'],

@@ -53,9 +53,12 @@ constexpr int kLdsListSlots = 8;          // LDS path: the first slots of every 
 #define IGM_PAIR_BATCH 4
 #endif
 #ifndef IGM_POP_PAIR_BATCH
-#define IGM_POP_PAIR_BATCH 8
+#define IGM_POP_PAIR_BATCH 4  // measured on config C with the occupancy below: 4 beats 8
 #endif
 constexpr int kPopPairBatch = IGM_POP_PAIR_BATCH;  // HBM engine: neighbours per batch (loads in flight together)
+#ifndef IGM_POP_FORCE_OCC
+#define IGM_POP_FORCE_OCC 6  // waves per SIMD the force kernel's registers must allow (6 beats 4, 5 and 8)
+#endif
 
 // LDS anneal kernel: neighbours per batch.  LDS latency is short and lists are short, so
 // the masked tail of a wide batch costs more than the extra loads in flight win
@@ -1255,7 +1258,9 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
 }
 
 // Verlet list of every bead slot of a flagged structure: the 27 cells around its cell,
-// each x-run of cells one contiguous slot range (visited in slot order)
+// each x-run of cells one contiguous slot range (visited in slot order).  (Staging the
+// block's neighbourhood -- one contiguous slot range -- in LDS was measured 18 % slower
+// on config C: the walk is VALU-bound, and 64 KB of LDS halves the occupancy.)
 __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
     int s, i;
     if (!pop_build_slot(A, &s, &i)) return;
@@ -1280,6 +1285,24 @@ __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
                });
     }
     A.nnb[base + i] = (uint16_t)(k <= kcap ? k : kNnbWalk);
+}
+
+// pair forces of a slot past the Verlet-list capacity: the 27 cells of the build-time
+// grid (a superset of its list, visited in slot order).  Out of line, with plain
+// arguments, so the rare path costs the hot force kernel no registers.
+__device__ __noinline__ float4 pop_walk_pairs(const float4* pos, const int* cell, const float* gp, const int* gn,
+                                              float bx, float by, float bz, int i, float4 p0, float evfpi) {
+    float fx = 0.0f, fy = 0.0f, fz = 0.0f;
+    walk27(cell_index<float>(bx, by, bz, gp, gp + 3, gn), cell, (const uint16_t*)nullptr, gn, [&](int j, bool ok) {
+        const float4 p = pos[j];
+        const float dx = p0.x - p.x, dy = p0.y - p.y, dz = p0.z - p.z;
+        const float f = soft_pair_bf(dx * dx + dy * dy + dz * dz, p0.w + p.w, evfpi);
+        const float m = (ok && j != i) ? f : 0.0f;
+        fx += m * dx;
+        fy += m * dy;
+        fz += m * dz;
+    });
+    return make_float4(fx, fy, fz, 0.0f);
 }
 
 // f32 force on slot i of structure s: the MD force path of atom_force specialised
@@ -1323,10 +1346,11 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     if (ri >= 0.0f) {
         if (nn == kNnbWalk) {
             const float4 b = A.xb[base + i];
-            const float* gp = A.gp + (size_t)s * 8;
-            const int* gn = A.gn + (size_t)s * 8;
-            walk27(cell_index<float>(b.x, b.y, b.z, gp, gp + 3, gn), A.cell + (size_t)s * kPopCells,
-                   (const uint16_t*)nullptr, gn, [&](int j, bool ok) { pair(pos[j], ok && j != i); });
+            const float4 f = pop_walk_pairs(pos, A.cell + (size_t)s * kPopCells, A.gp + (size_t)s * 8,
+                                            A.gn + (size_t)s * 8, b.x, b.y, b.z, i, p0, evfpi);
+            fx = f.x;
+            fy = f.y;
+            fz = f.z;
         } else {
             for (int k0 = 0; k0 < nn; k0 += U) {
                 int jt[U];
@@ -1387,7 +1411,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 
 // forces of every slot (+ final_integrate and this block's kinetic-energy partial
 // when S.integrate; the run's setup evaluation otherwise)
-__global__ void __launch_bounds__(kPopBS) pop_force_kernel(PopArgs A, float evf, float envf, PopStep S) {
+__global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(PopArgs A, float evf, float envf, PopStep S) {
     __shared__ double red[kPopBS / 64];
     const int lb = pop_block(), s = lb / A.nbs, blk = lb % A.nbs, i = blk * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
@@ -2378,13 +2402,8 @@ int prepare(igm_ctx* c, uint32_t flags, const igm_mstep_params* prm, int32_t nst
     out->cm.kcap = kcap;
     LaunchCfg cfg;
     out->big = (prm->flags & IGM_MSTEP_FORCE_GLOBAL) || getenv("IGM_FORCE_POP") || !lds_fits(natom, &cfg);
-    if (out->big && !(prm->skin > 0) && !getenv("IGM_SKIN_FACTOR")) {
-        // the HBM engine gathers neighbours from L2/MALL: a tighter list (skin 0.55
-        // maxrad, scripts/gpu_skin.sh on config C) beats the extra rebuilds
-        const float rmax = 0.5f * (P.cut_list - P.skin);
-        P.skin = 0.55f * rmax;
-        P.cut_list = 2.0f * rmax + P.skin;
-    }
+    // (the population engine's skin optimum is also 0.7 maxrad: config C, protocol x0.2,
+    //  0.45 / 0.55 / 0.7 / 0.85 / 1.0 maxrad -> 5.59 / 5.45 / 5.31 / 5.32 / 5.37 s anneal)
     out->P = P;
     return IGM_OK;
 }

@@ -75,6 +75,6 @@ def relax_population(cfg, xyz, radii, chrom, copy, struct_ids, volumes=None, vol
     x = np.zeros((len(struct_ids), atoms.n, 3), np.float32)
     x[:, :nb] = xyz
     opt = cfg['optimization']['optimizer_options']
-    seeds = M.lammps_seeds(opt.get('seed', 6535), struct_ids, cfg.get('runtime', {}).get('step_no', 0))
+    seeds = M.lammps_seeds(opt.get('seed', 6535), struct_ids, cfg.get('runtime', {}).get('step_no', 1))  # lammps.py:435
     xo, info = mstep.run(prm, x, atoms.radii, atoms.flags, poly, None, None, seeds, ctx=c)
     return xo[:, :nb], info

@@ -35,15 +35,26 @@ def shard(n, rank, world):
     return n * rank // world, n * (rank + 1) // world
 
 
+def _staged(t, group):
+    """gloo moves host tensors only: device tensors go through host memory (the
+    functional multi-process path on one GPU and the CPU tests); RCCL ('nccl') keeps
+    them in HBM."""
+    import torch.distributed as dist
+    return t.is_cuda and dist.get_backend(group) == 'gloo'
+
+
 def gather_population(xyz_local, group=None):
     """Every rank's (S_local, natom, 3) block -> the (S_total, natom, 3) population
     in rank order (one all-gather; RCCL over xGMI on the GPUs)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    parts = [torch.empty_like(xyz_local) for _ in range(world)]
-    dist.all_gather(parts, xyz_local.contiguous(), group=group)
-    return torch.cat(parts, 0)
+    host = _staged(xyz_local, group)
+    src = xyz_local.contiguous().cpu() if host else xyz_local.contiguous()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src, group=group)
+    out = torch.cat(parts, 0)
+    return out.to(xyz_local.device) if host else out
 
 
 def gather_rows(rows_u8, nrows, itemsize, group=None):
@@ -53,24 +64,30 @@ def gather_rows(rows_u8, nrows, itemsize, group=None):
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    host = _staged(rows_u8, group)
     dev = rows_u8.device
-    counts = torch.tensor([int(nrows)], dtype=torch.int64, device=dev)
+    cdev = torch.device('cpu') if host else dev
+    counts = torch.tensor([int(nrows)], dtype=torch.int64, device=cdev)
     allc = [torch.zeros_like(counts) for _ in range(world)]
     dist.all_gather(allc, counts, group=group)
     allc = [int(x.item()) for x in allc]
     mx = max(max(allc), 1)
-    buf = torch.zeros(mx * itemsize, dtype=torch.uint8, device=dev)
-    buf[:nrows * itemsize] = rows_u8[:nrows * itemsize]
+    buf = torch.zeros(mx * itemsize, dtype=torch.uint8, device=cdev)
+    buf[:nrows * itemsize] = rows_u8[:nrows * itemsize].to(cdev)
     bufs = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(bufs, buf, group=group)
-    return torch.cat([b[:c * itemsize] for b, c in zip(bufs, allc)]), sum(allc)
+    out = torch.cat([b[:c * itemsize] for b, c in zip(bufs, allc)])
+    return (out.to(dev) if host else out), sum(allc)
 
 
 def reduce_sum_f64(values, device, group=None):
     """Sum a few host numbers over the ranks (violation counts of log_stats)."""
     import torch
     import torch.distributed as dist
-    v = torch.tensor(values, dtype=torch.float64, device=device)
+    dev = torch.device(device)
+    if dev.type == 'cuda' and dist.get_backend(group) == 'gloo':
+        dev = torch.device('cpu')
+    v = torch.tensor(values, dtype=torch.float64, device=dev)
     dist.all_reduce(v, group=group)
     return v.cpu().numpy()
 

@@ -1,0 +1,505 @@
+"""Drop-in Step layer for igm-run: ActivationDistanceStep and
+ModelingStep with the reference's Step plugin contract, run by a per-GPU batch
+scheduler instead of ipyparallel, restartable at batch granularity.
+
+  StepDB          igm/core/job_tracking.py:9-123 -- the same sqlite file and schema
+                  (table `steps`: uid, name, cfg, time, status, data), so igm-run's
+                  restart logic reads our records unchanged.
+  Step            igm/core/step.py:23-328 -- the same lifecycle and status rows
+                  (entry, setup, map, mapped, reduced, cleanup, completed, failed),
+                  uid = md5('<name>:<step_no>'), a completed step is skipped, a
+                  failure is recorded with its traceback and re-raised.
+  BatchScheduler  replaces Controller.map (parallel/ipyparallel_controller.py:61-109):
+                  argument_list entries are BATCHES (thousands of structures or pairs
+                  per GPU call, not one structure per process); one worker thread per
+                  GPU, each with its own igm_ctx; a batch's completion is recorded
+                  (<uid>.batch<k>.done, written by atomic rename after the batch's
+                  outputs) in place of the per-structure '<uid>.<sid>.ready' files
+                  (ModelingStep.py:178-183), and a restarted map skips every batch
+                  that has one.
+  ActivationDistanceStep / ModelingStep
+                  the A-step (ActivationDistanceStep.py:42-298) and M-step
+                  (ModelingStep.py:105-783) on the GPU kernels of this package.
+
+Storage.  The reference keeps the population in alabtools' .hss (HDF5) and the
+rows in actdist.hdf5; h5py is not importable by this package's Python, so the same
+arrays live in numpy files with the reference's layouts: `<structure_output>.npy`
+= the .hss 'coordinates' dataset (nbead, nstruct, 3) float32 (bead-major), with the
+index / radii in `<structure_output>.index.npz`; `actdist.npz` = {row, col, dist,
+prob} of actdist.hdf5.  The kernels behind the steps are looked up by name in
+KERNELS (cfg optimization/kernel, default 'hip'); the product registers only the
+GPU kernels.
+"""
+import hashlib
+import json
+import os
+import sqlite3
+import threading
+import time
+import traceback
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import model as M
+from ._lib import pair_dtype, row_dtype
+
+
+# ------------------------------------------------------------------ config helpers
+def cget(cfg, key, default=None):
+    """Config.get keypath semantics (core/config.py:98-127) on a plain dict."""
+    d = cfg
+    for k in key.split('/'):
+        if not isinstance(d, dict) or k not in d:
+            return default
+        d = d[k]
+    return d
+
+
+def cset(cfg, key, value):
+    ks = key.split('/')
+    d = cfg
+    for k in ks[:-1]:
+        d = d.setdefault(k, {})
+    d[ks[-1]] = value
+
+
+def _json_default(o):
+    if isinstance(o, np.generic):
+        return o.item()
+    if isinstance(o, np.ndarray):
+        return o.tolist()
+    raise TypeError(type(o))
+
+
+# ------------------------------------------------------------------ StepDB
+class StepDB(object):
+    """igm.core.job_tracking.StepDB: sqlite table `steps`, json columns cfg / data."""
+    SCHEMA = [('uid', 'TEXT'), ('name', 'TEXT'), ('cfg', 'TEXT'), ('time', 'INT'), ('status', 'TEXT'),
+              ('data', 'TEXT')]
+    JSONCOLS = ('cfg', 'data')
+    COLUMNS = [x[0] for x in SCHEMA]
+
+    def __init__(self, cfg):
+        self.db = cfg if isinstance(cfg, str) else cget(cfg, 'parameters/step_db', None)
+        if self.db and not os.path.isfile(self.db):
+            with sqlite3.connect(self.db) as conn:
+                conn.execute('CREATE TABLE steps (' + ','.join(' '.join(x) for x in self.SCHEMA) + ')')
+        elif self.db:
+            with sqlite3.connect(self.db) as conn:
+                s = conn.execute('PRAGMA table_info(steps)').fetchall()
+            for i, (n, t) in enumerate(self.SCHEMA):
+                if i >= len(s) or s[i][1] != n or s[i][2] != t:
+                    raise AssertionError('Invalid database file %s (column %d)' % (self.db, i))
+
+    def record(self, **kw):
+        if not self.db:
+            return
+        row = []
+        for c, _ in self.SCHEMA:
+            if c == 'time':
+                row.append(kw.get('time', time.time()))
+            elif c in self.JSONCOLS:
+                row.append(json.dumps(kw.get(c, None), default=_json_default))
+            else:
+                row.append(kw.get(c, ''))
+        with sqlite3.connect(self.db) as conn:
+            conn.execute('INSERT INTO steps (%s) VALUES (%s)' % (','.join(self.COLUMNS), ','.join('?' * len(row))),
+                         tuple(row))
+
+    def get_history(self, uid=None):
+        if not self.db:
+            return []
+        with sqlite3.connect(self.db) as conn:
+            if uid is None:
+                r = conn.execute('SELECT * FROM steps ORDER BY time').fetchall()
+            else:
+                r = conn.execute('SELECT * FROM steps WHERE uid=? ORDER BY time', (uid,)).fetchall()
+        return [{c: (json.loads(v) if c in self.JSONCOLS else v) for c, v in zip(self.COLUMNS, x)} for x in r]
+
+
+# ------------------------------------------------------------------ scheduler
+class BatchScheduler(object):
+    """Per-GPU batch scheduler: map(task, batches) runs task(batch, device) for every
+    batch not yet recorded as done, one worker thread per device (each thread owns
+    its device's igm_ctx: _lib.context(device)).  A batch is done once task returned
+    and its record was renamed into place; the first failing batch stops the map and
+    re-raises (the reference's remote-failure abort, ipyparallel_controller.py:92-97),
+    after the batches already running have finished and been recorded."""
+
+    def __init__(self, devices=(0,), record_dir='.', uid='step', clean_restart=False):
+        self.devices = list(devices) or [0]
+        self.record_dir = record_dir
+        self.uid = uid
+        if clean_restart:
+            for f in os.listdir(record_dir):
+                if f.startswith(uid + '.batch') and f.endswith('.done'):
+                    os.remove(os.path.join(record_dir, f))
+
+    def record_path(self, k):
+        return os.path.join(self.record_dir, '%s.batch%d.done' % (self.uid, k))
+
+    def done(self, k):
+        return os.path.isfile(self.record_path(k))
+
+    def _record(self, k, info):
+        tmp = self.record_path(k) + '.tmp'
+        with open(tmp, 'w') as f:
+            json.dump(info, f, default=_json_default)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self.record_path(k))
+
+    def map(self, task, batches):
+        pending = [k for k in range(len(batches)) if not self.done(k)]
+        lock = threading.Lock()
+        queue = list(pending)
+        errors = []
+        ran = []
+
+        def worker(dev):
+            while True:
+                with lock:
+                    if errors or not queue:
+                        return
+                    k = queue.pop(0)
+                t0 = time.time()
+                try:
+                    task(batches[k], dev)
+                except BaseException as e:  # noqa: B902 -- recorded, then re-raised by map()
+                    with lock:
+                        errors.append((k, e, traceback.format_exc()))
+                    return
+                self._record(k, {'batch': k, 'device': dev, 'seconds': time.time() - t0})
+                with lock:
+                    ran.append(k)
+
+        with ThreadPoolExecutor(max_workers=len(self.devices)) as ex:
+            list(ex.map(worker, self.devices))
+        if errors:
+            k, e, tb = min(errors, key=lambda x: x[0])
+            raise RuntimeError('batch %d failed: %s\n%s' % (k, e, tb))
+        return sorted(ran)
+
+
+# ------------------------------------------------------------------ Step
+class Step(object):
+    """igm.core.step.Step with the same run() semantics; argument_list holds batches."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.tmp_extensions = []
+        workdir = cget(cfg, 'parameters/workdir', '.')
+        tmp = cget(cfg, 'parameters/tmp_dir', 'tmp/')
+        self.tmp_dir = tmp if os.path.isabs(tmp) else os.path.join(workdir, tmp)
+        self.keep_temporary_files = True
+        os.makedirs(self.tmp_dir, exist_ok=True)
+        rt = cfg.setdefault('runtime', {})
+        if 'current_iteration_name' not in rt:
+            rt['current_iteration_name'] = self.name()
+        if rt.get('step_no') is None:
+            rt['step_no'] = -1
+        rt['step_no'] += 1
+        self._db = StepDB(cfg)
+        self.uid = hashlib.md5('{:s}:{:d}'.format(self.name(), rt['step_no']).encode()).hexdigest()
+        rt['step_hash'] = self.uid
+        self.argument_list = []
+        self.mapped_batches = []
+
+    # overridables
+    def setup(self):
+        self.argument_list = []
+
+    def before_map(self):
+        return
+
+    def task(self, batch, device):
+        raise NotImplementedError
+
+    def before_reduce(self):
+        return
+
+    def reduce(self):
+        return
+
+    def cleanup(self):
+        if not self.keep_temporary_files:
+            for f in os.listdir(self.tmp_dir):
+                if os.path.splitext(f)[1] in self.tmp_extensions:
+                    os.remove(os.path.join(self.tmp_dir, f))
+
+    def skip(self):
+        return None
+
+    def name(self):
+        return self.__class__.__name__
+
+    def scheduler(self):
+        hip = cget(self.cfg, 'optimization/kernel_opts/hip', {}) or {}
+        return BatchScheduler(hip.get('devices', [0]), self.tmp_dir, self.uid,
+                              clean_restart=bool(cget(self.cfg, 'optimization/clean_restart', False)))
+
+    def run(self):
+        """core/step.py:226-322, DO NOT OVERLOAD."""
+        dbdata = {'uid': self.uid, 'name': self.name(), 'cfg': self.cfg}
+        past = {x['status']: x['cfg'] for x in self._db.get_history(self.uid)}
+        if 'completed' in past:
+            self.cfg['runtime'].update(past['completed']['runtime'])
+            self.skip()
+            return
+        try:
+            dbdata['status'] = 'entry'
+            self._db.record(**dbdata)
+            self.setup()
+            dbdata['status'] = 'setup'
+            self._db.record(**dbdata)
+            if 'mapped' not in past:
+                self.before_map()
+                dbdata['status'] = 'map'
+                self._db.record(**dbdata)
+                self.mapped_batches = self.scheduler().map(self.task, self.argument_list)
+                dbdata['status'] = 'mapped'
+                self._db.record(**dbdata)
+            else:
+                self.cfg['runtime'].update(past['mapped']['runtime'])
+            if 'reduced' not in past:
+                self.before_reduce()
+                self.reduce()
+                dbdata['status'] = 'reduced'
+                self._db.record(**dbdata)
+            else:
+                self.cfg['runtime'].update(past['reduced']['runtime'])
+            if 'cleanup' not in past:
+                self.cleanup()
+                dbdata['status'] = 'cleanup'
+                self._db.record(**dbdata)
+            else:
+                self.cfg['runtime'].update(past['cleanup']['runtime'])
+            dbdata['status'] = 'completed'
+            self.cfg['runtime'].pop('step_hash', None)
+            self._db.record(**dbdata)
+        except BaseException:
+            dbdata['status'] = 'failed'
+            dbdata['data'] = {'exception': traceback.format_exc()}
+            self._db.record(**dbdata)
+            raise
+
+
+# ------------------------------------------------------------------ population store
+class PopulationStore(object):
+    """The .hss arrays the steps read and write: coordinates (nbead, nstruct, 3) float32
+    bead-major (core/step.py:373, _preprocess.py:103-105) as a memory-mapped .npy, and
+    the index (radii, chrom, copy, copy_ptr/copy_idx of index.copy_index, chrom_sizes)."""
+
+    def __init__(self, path):
+        self.path = path
+        meta = np.load(path + '.index.npz')
+        self.radii = meta['radii'].astype(np.float32)
+        self.chrom = meta['chrom'].astype(np.int32)
+        self.copy = meta['copy'].astype(np.int32)
+        self.copy_ptr = meta['copy_ptr'].astype(np.int32)
+        self.copy_idx = meta['copy_idx'].astype(np.int32)
+        self.hap_chrom = meta['hap_chrom'].astype(np.int32) if 'hap_chrom' in meta else self.chrom
+        self.nbead = len(self.radii)
+
+    @staticmethod
+    def create(path, coordinates, radii, chrom, copy, copy_ptr, copy_idx, hap_chrom=None):
+        np.savez(path + '.index.npz', radii=radii, chrom=chrom, copy=copy, copy_ptr=copy_ptr, copy_idx=copy_idx,
+                 hap_chrom=chrom if hap_chrom is None else hap_chrom)
+        np.save(path + '.npy', np.ascontiguousarray(coordinates, np.float32))
+        return PopulationStore(path)
+
+    def coordinates(self, mode='r'):
+        return np.load(self.path + '.npy', mmap_mode=mode)
+
+    @property
+    def nstruct(self):
+        return self.coordinates().shape[1]
+
+
+# ------------------------------------------------------------------ kernels
+def _hip_actdist(store, pairs, cfg, device):
+    from . import astep, _lib
+    xyz = np.ascontiguousarray(store.coordinates())
+    return astep.compute_actdist(xyz, store.radii, store.copy_ptr, store.copy_idx, store.hap_chrom, pairs,
+                                 float(cget(cfg, 'restraints/Hi-C/contact_range', 2.0)),
+                                 int(cget(cfg, 'runtime/Hi-C/iter_corr_knob', 1)), ctx=_lib.context(device))
+
+
+def _hip_mstep(store, sids, rows, cfg, device):
+    """ModelingStep.task for a batch of structures on one GPU: Hi-C selection, the
+    annealing protocol + CG, violation records.  Returns dict(xyz (S, nbead, 3) f32,
+    info (S) optinfo, stats (S, ncls, 104))."""
+    from . import mstep, _lib
+    ctx = _lib.context(device)
+    prm, atoms, poly, chrom, cr, k, env_scale = modeling_inputs(store, cfg)
+    crd = store.coordinates()
+    x = np.zeros((len(sids), atoms.n, 3), np.float32)
+    x[:, :atoms.nbead] = np.asarray(crd[:, sids, :]).transpose(1, 0, 2)
+    ptr, bonds, bcls = mstep.hic_select(x, atoms.radii, chrom, rows['row'], rows['col'], rows['dist'], cr, k,
+                                        ctx=ctx)
+    seeds = M.lammps_seeds(cget(cfg, 'optimization/optimizer_options/seed', 6535), sids,
+                           cget(cfg, 'runtime/step_no', 1))
+    xo, info = mstep.run(prm, x, atoms.radii, atoms.flags, poly, ptr, bonds, seeds, ctx=ctx)
+    stats = mstep.violations(prm, xo, atoms.radii, atoms.flags, poly, np.full(len(poly), M.CLASS_POLYMER, np.int32),
+                             ptr, bonds, bcls, [cr, cr, cr], env_scale,
+                             float(cget(cfg, 'optimization/violation_tolerance', 0.05)), ctx=ctx)
+    return {'xyz': xo[:, :atoms.nbead], 'info': info, 'stats': stats}
+
+
+KERNELS = {'hip': {'actdist': _hip_actdist, 'mstep': _hip_mstep}}
+
+
+def modeling_inputs(store, cfg):
+    """The per-batch model of ModelingStep.task (Hi-C configuration): steric + polymer +
+    sphere/ellipsoid envelope, params of optimization/optimizer_options."""
+    rs = cget(cfg, 'model/restraints', {})
+    env = rs.get('envelope', {'nucleus_shape': 'sphere', 'nucleus_radius': 5500.0, 'nucleus_kspring': 1.0})
+    if env['nucleus_shape'] == 'sphere':
+        abc = (float(env['nucleus_radius']),) * 3
+    else:
+        abc = tuple(float(v) for v in env['nucleus_semiaxes'])
+    kenv = float(env.get('nucleus_kspring', 1.0))
+    poly_cfg = rs.get('polymer', {'contact_range': 2.0, 'polymer_kspring': 1.0})
+    poly = M.polymer_bonds(store.chrom, store.copy, store.radii, poly_cfg['contact_range'],
+                           poly_cfg['polymer_kspring'])
+    atoms = M.Atoms(store.radii)
+    prm = M.params_from_cfg(cfg, [(abc, kenv)], evfactor=float(rs.get('excluded', {}).get('evfactor', 1.0)))
+    chrom = np.concatenate([store.chrom, [-1]]).astype(np.int32)
+    hic = cget(cfg, 'restraints/Hi-C', {})
+    return (prm, atoms, poly, chrom, float(hic.get('contact_range', 2.0)), float(hic.get('contact_kspring', 1.0)),
+            [0.1 * float(np.mean(abc))])
+
+
+def _kernel(cfg, what):
+    name = cget(cfg, 'optimization/kernel', 'hip')
+    if name not in KERNELS:
+        raise ValueError('optimization/kernel %r is not registered (have %s)' % (name, sorted(KERNELS)))
+    return KERNELS[name][what]
+
+
+# ------------------------------------------------------------------ the steps
+class ActivationDistanceStep(Step):
+    """ActivationDistanceStep.py:42-298 with the pair batches on the GPUs."""
+
+    def __init__(self, cfg):
+        rt = cfg.setdefault('runtime', {}).setdefault('Hi-C', {})
+        hic = cfg['restraints']['Hi-C']
+        rt.setdefault('intra_sigma_list', list(hic['intra_sigma_list']))
+        rt.setdefault('inter_sigma_list', list(hic['inter_sigma_list']))
+        if 'iter_corr_knob' not in rt:  # D1: absent from the schema, default 1
+            rt['iter_corr_knob'] = cget(cfg, 'optimization/iter_corr_knob', 1)
+        if 'inter_sigma' not in rt and 'intra_sigma' not in rt:
+            if len(rt['inter_sigma_list']) and len(rt['intra_sigma_list']):
+                rt['inter_sigma'] = rt['inter_sigma_list'].pop(0)
+                rt['intra_sigma'] = rt['intra_sigma_list'].pop(0)
+        super(ActivationDistanceStep, self).__init__(cfg)
+
+    def name(self):
+        return 'ActivationDistanceStep (INTER sigma={:.2f}%, INTRA sigma={:.2f}%, iter={:s})'.format(
+            cget(self.cfg, 'runtime/Hi-C/inter_sigma') * 100.0, cget(self.cfg, 'runtime/Hi-C/intra_sigma') * 100.0,
+            str(cget(self.cfg, 'runtime/opt_iter', 'NA')))
+
+    def setup(self):
+        from . import astep
+        hic = np.load(self.cfg['restraints']['Hi-C']['input_matrix'])  # .hcs arrays: indptr, indices, data, chrom
+        last = cget(self.cfg, 'runtime/Hi-C/actdist_file', None)
+        last_rows = None
+        if last is not None and os.path.isfile(last):
+            d = np.load(last)
+            last_rows = np.zeros(len(d['row']), row_dtype)
+            for k in ('row', 'col', 'dist', 'prob'):
+                last_rows[k] = d[k]
+        pairs = astep.select_pairs(hic['indptr'], hic['indices'], hic['data'], hic['chrom'],
+                                   cget(self.cfg, 'runtime/Hi-C/intra_sigma', False),
+                                   cget(self.cfg, 'runtime/Hi-C/inter_sigma', False), last_rows=last_rows)
+        bs = int(cget(self.cfg, 'optimization/kernel_opts/hip/pair_batch', 1 << 20))
+        self.argument_list = []
+        for b, q0 in enumerate(range(0, max(len(pairs), 1), bs)):
+            fn = os.path.join(self.tmp_dir, '%s.%d.in.npy' % (self.uid, b))
+            np.save(fn, pairs[q0:q0 + bs])
+            self.argument_list.append({'batch': b, 'pairs': fn,
+                                       'out': os.path.join(self.tmp_dir, '%s.%d.rows.npy' % (self.uid, b))})
+        self.tmp_extensions = ['.npy']
+
+    def task(self, batch, device):
+        store = PopulationStore(self.cfg['optimization']['structure_output'])
+        pairs = np.load(batch['pairs'])
+        rows = _kernel(self.cfg, 'actdist')(store, pairs, self.cfg, device)
+        tmp = batch['out'] + '.part.npy'
+        np.save(tmp, rows)
+        os.replace(tmp, batch['out'])
+
+    def reduce(self):
+        """concatenate in batch order (= CSR pair order) -> actdist.npz; the previous
+        file is rotated like ActivationDistanceStep.py:292-295."""
+        rows = np.concatenate([np.load(b['out']) for b in self.argument_list]) if self.argument_list else \
+            np.zeros(0, row_dtype)
+        out = os.path.join(cget(self.cfg, 'parameters/workdir', '.'),
+                           cget(self.cfg, 'restraints/Hi-C/actdist_file', 'actdist.npz'))
+        last = cget(self.cfg, 'runtime/Hi-C/actdist_file', None)
+        if last is not None and os.path.isfile(last) and os.path.abspath(last) == os.path.abspath(out):
+            os.replace(last, '%s.INTERsigma_%.4f_INTRAsigma_%.4f_iter_%s' % (
+                out, cget(self.cfg, 'runtime/Hi-C/inter_sigma'), cget(self.cfg, 'runtime/Hi-C/intra_sigma'),
+                str(cget(self.cfg, 'runtime/opt_iter', 0))))
+        tmp = out + '.part.npz'
+        np.savez(tmp, row=rows['row'], col=rows['col'], dist=rows['dist'], prob=rows['prob'])
+        os.replace(tmp, out)
+        cset(self.cfg, 'runtime/Hi-C/actdist_file', out)
+
+
+class ModelingStep(Step):
+    """ModelingStep.py:105-783 with batches of structures on the GPUs; the per-batch
+    records replace the '.ready' files and the FilePoller."""
+
+    def setup(self):
+        S = int(self.cfg['model']['population_size'])
+        bs = int(cget(self.cfg, 'optimization/kernel_opts/hip/batch_size', 1000))
+        self.argument_list = [{'batch': b, 'sids': list(range(s0, min(s0 + bs, S))),
+                               'out': os.path.join(self.tmp_dir, '%s.%d.mstep.npz' % (self.uid, b))}
+                              for b, s0 in enumerate(range(0, S, bs))]
+        self.tmp_extensions = ['.npz']
+
+    def task(self, batch, device):
+        store = PopulationStore(self.cfg['optimization']['structure_output'])
+        act = cget(self.cfg, 'runtime/Hi-C/actdist_file', None)
+        d = np.load(act) if act else None
+        rows = np.zeros(0 if d is None else len(d['row']), row_dtype)
+        if d is not None:
+            for k in ('row', 'col', 'dist', 'prob'):
+                rows[k] = d[k]
+        res = _kernel(self.cfg, 'mstep')(store, np.asarray(batch['sids']), rows, self.cfg, device)
+        tmp = batch['out'] + '.part.npz'
+        np.savez(tmp, xyz=res['xyz'], info=res['info'].view(np.uint8), stats=res['stats'])
+        os.replace(tmp, batch['out'])
+
+    def reduce(self):
+        """set_structure for every structure + teardown_poller + log_stats
+        (ModelingStep.py:612-746): coordinates into the population, the summary JSON,
+        runtime/violation_score."""
+        from ._lib import optinfo_dtype
+        from .summary import PopulationSummary, vstat_from_record, restraint_key
+        store = PopulationStore(self.cfg['optimization']['structure_output'])
+        crd = store.coordinates('r+')
+        summ = PopulationSummary(crd.shape[1])
+        env = cget(self.cfg, 'model/restraints/envelope', {'nucleus_shape': 'sphere', 'nucleus_radius': 5500.0,
+                                                           'nucleus_kspring': 1.0})
+        # vstat keys: repr() of the reference restraints, the config's numbers as written
+        abc = [env.get('nucleus_radius')] * 3 if env['nucleus_shape'] == 'sphere' else env['nucleus_semiaxes']
+        names = ['Polymer', 'interHiC', 'intraHiC',
+                 restraint_key('Envelope', shape=env['nucleus_shape'], k=env.get('nucleus_kspring', 1.0),
+                               a=abc[0], b=abc[1], c=abc[2])]
+        for b in self.argument_list:
+            res = np.load(b['out'])
+            info = res['info'].view(optinfo_dtype)
+            for q, sid in enumerate(b['sids']):
+                crd[:, sid, :] = res['xyz'][q]
+                opt = {'final-energy': float(info['final_energy'][q]), 'pair-energy': float(info['pair_energy'][q]),
+                       'bond-energy': float(info['bond_energy'][q]),
+                       'thermo': {'Temp': float(info['temp'][q])}}
+                summ.set_structure(sid, vstat_from_record(res['stats'][q], names), opt)
+        crd.flush()
+        del crd
+        with open(self.cfg['optimization']['structure_output'] + '.summary.json', 'w') as f:
+            f.write(summ.to_json())
+        cset(self.cfg, 'runtime/violation_score', float(summ.violation_score()))
