@@ -53,9 +53,9 @@ constexpr int kLdsListSlots = 8;          // LDS path: the first slots of every 
 #define IGM_PAIR_BATCH 4
 #endif
 #ifndef IGM_POP_PAIR_BATCH
-#define IGM_POP_PAIR_BATCH 4  // measured on config C with the occupancy below: 4 beats 8
+#define IGM_POP_PAIR_BATCH 1  // list quads (4 neighbours each) per batch of the population engine
 #endif
-constexpr int kPopPairBatch = IGM_POP_PAIR_BATCH;  // HBM engine: neighbours per batch (loads in flight together)
+constexpr int kPopPairBatch = IGM_POP_PAIR_BATCH;  // population engine: list quads whose loads are in flight together
 #ifndef IGM_POP_FORCE_OCC
 #define IGM_POP_FORCE_OCC 6  // waves per SIMD the force kernel's registers must allow (6 beats 4, 5 and 8)
 #endif
@@ -220,7 +220,7 @@ __host__ __device__ inline size_t carve_ws(void* base, int natom, int ldn, int k
     L->cell = cv.take<int>(cellcap + 8);
     L->nnb = cv.take<uint16_t>(ldn);
     L->sorted = cv.take<uint16_t>(ldn);
-    L->gell = cv.take<uint16_t>((size_t)ldn * kg + 64 * kPopPairBatch);  // slack for the batched reads
+    L->gell = cv.take<uint16_t>((size_t)ldn * kg + 64 * IGM_PAIR_BATCH);  // slack for the batched reads
     L->kg = kg;
     L->lell = nullptr;
     L->lstride = 0;
@@ -901,6 +901,12 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
 constexpr int kPopBS = 256;
 constexpr int kPopSortNT = 1024;
 constexpr int kPopCells = kCellCapBig + 2;  // cell offsets of a structure: real cells, non-bead run, end
+#ifndef IGM_POP_FILL_W
+#define IGM_POP_FILL_W 4
+#endif
+constexpr int kFillW = IGM_POP_FILL_W;  // list build: slots per x-run loaded in one batch
+constexpr int kPopListCap = 64;          // Verlet-list entries per slot (more: the cell walk)
+constexpr int kPopListRow = kPopListCap + 2;  // u16 per LDS list row of the build (odd word stride)
 
 struct PopBuf {
     float4* pos;   // (B, ldn): x, y, z, w = radius (bead) or -(radius + 1)
@@ -916,7 +922,7 @@ struct PopArgs {
     PopBuf buf[2];
     int* par;            // (B) buffer holding the current slot order
     float4* xb;          // (B, ldn) position of the slot at its list build
-    uint16_t* nl;        // (B, nslice, kcap, 64) Verlet list, slot ids
+    uint2* nl;           // (B, nslice, kq, 64) Verlet list: quads of u16 slot ids, padded with the own slot
     uint16_t* nnb;       // (B, ldn) list length, or kNnbWalk
     int* cell;           // (B, kPopCells) first slot of every cell of the build grid
     float* gp;           // (B, 8) grid lo[3], inv[3]
@@ -924,6 +930,7 @@ struct PopArgs {
     uint32_t* bent;      // (B, nslice, bdmax, 64) bonds of a slot: partner slot | type << 16 | lower << 31
     uint16_t* bdeg;      // (B, ldn)
     int bdmax;
+    int kq;              // list quads per slot (4 kq >= the Verlet-list capacity)
     int* flag;           // (B) list rebuild needed
     int* flist;          // (B) the flagged structures of this step, compacted
     int* nflag;          // (1)
@@ -1066,7 +1073,11 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
 // sort (ascending ids: deterministic) never leave the CU.  Non-bead atoms form a last
 // run after the real cells.  Writes the new slot order (aid, slot) and the cell
 // offsets, and flips the structure's parity.
-template <bool IDS_LDS>
+//   APT > 0: every thread keeps the (cell, rank) of its APT atoms (t + u * kPopSortNT,
+// N <= APT * kPopSortNT) in registers, and all their loads are in flight together --
+// the sort is one workgroup's chain of dependent memory round trips, so fewer and
+// wider trips are what makes it faster.
+template <bool IDS_LDS, int APT>
 __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cw[];  // (kPopCells + 1) / 2 words, then ids
     __shared__ int wsum[kMaxWaves];
@@ -1129,6 +1140,28 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A) {
     for (int k = t; k < nw; k += kPopSortNT) cw[k] = 0u;
     __syncthreads();
     constexpr int U = 4;  // independent loads in flight per thread
+    uint32_t cr[APT > 0 ? APT : 1];
+    if constexpr (APT > 0) {
+#pragma unroll
+        for (int u0 = 0; u0 < APT; u0 += 8) {
+            float4 pp[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = t + (u0 + u) * kPopSortNT;
+                pp[u] = pos[i < N ? i : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = t + (u0 + u) * kPopSortNT;
+                if (u0 + u < APT && i < N) {
+                    const int c = pp[u].w >= 0.0f ? cell_index<float>(pp[u].x, pp[u].y, pp[u].z, lo, inv, nb) : ncell;
+                    const uint32_t sh = (uint32_t)(c & 1) << 4;
+                    const uint32_t old = atomicAdd(&cw[c >> 1], 1u << sh);
+                    cr[u0 + u] = ((uint32_t)c << 16) | ((old >> sh) & 0xffffu);
+                }
+            }
+        }
+    } else
     for (int i0 = t; i0 < N; i0 += U * kPopSortNT) {
         float4 pp[U];
 #pragma unroll
@@ -1177,6 +1210,17 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A) {
             aidn[k] = v;
     };
     auto get = [&](int k) -> int { return IDS_LDS ? (int)ids[k] : aidn[k]; };
+    if constexpr (APT > 0) {
+        int aa[APT];
+#pragma unroll
+        for (int u = 0; u < APT; ++u) {
+            const int i = t + u * kPopSortNT;
+            aa[u] = aido[i < N ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < APT; ++u)
+            if (t + u * kPopSortNT < N) put(off((int)(cr[u] >> 16)) + (int)(cr[u] & 0xffffu), aa[u]);
+    } else
     for (int i0 = t; i0 < N; i0 += U * kPopSortNT) {
         uint32_t uu[U];
         int aa[U];
@@ -1241,7 +1285,7 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     const float4 x = O.pos[o];
     B.pos[k] = x;
     B.vel[k] = O.vel[o];
-    B.frc[k] = O.frc[o];
+    // (no force: the force kernel of this step rewrites every slot's before any read)
     A.xb[k] = make_float4(x.x, x.y, x.z, 0.f);
     // the atom's bonds (sorted adjacency of prepare()) with partners as slots
     const Bonds& Bd = A.cm.bonds;
@@ -1250,41 +1294,123 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     const uint32_t* g = Bd.ent + Bd.base[s] + Bd.soff[(size_t)s * (nsl + 1) + (a >> 6)] + (a & 63);
     uint32_t* d = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const int* sl = B.slot + base;
-    for (int e = 0; e < deg; ++e) {
-        const uint32_t v = g[(size_t)e * 64];
-        d[(size_t)e * 64] = (v & 0xffff0000u) | (uint32_t)sl[v & 0xffffu];
+    for (int e0 = 0; e0 < deg; e0 += 4) {  // 4 entries, then their 4 slots, in flight together
+        uint32_t v[4];
+        int t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = g[(size_t)min(e0 + u, deg - 1) * 64];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[u] = sl[v[u] & 0xffffu];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (e0 + u < deg) d[(size_t)(e0 + u) * 64] = (v[u] & 0xffff0000u) | (uint32_t)t[u];
     }
     A.bdeg[k] = (uint16_t)deg;
 }
 
+
+typedef float pop_f2 __attribute__((ext_vector_type(2)));
+
+// slot j of a structure's float4 array through a buffer resource: a 32-bit offset and
+// no 64-bit address arithmetic per gather.  The array is the same for the whole wave
+// (one structure per block); readfirstlane says so, or every load becomes a waterfall.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pop_rsrc(const float4* p, int n) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* u = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(u, (short)0, __builtin_amdgcn_readfirstlane(n * 16), 0x00020000);
+}
+__device__ __forceinline__ float3 pop_ld3(__amdgpu_buffer_rsrc_t r, uint32_t j) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, j * 16u, 0, 0);
+    return make_float3(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]));
+}
+__device__ __forceinline__ float4 pop_ld(__amdgpu_buffer_rsrc_t r, uint32_t j) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, j * 16u, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+
 // Verlet list of every bead slot of a flagged structure: the 27 cells around its cell,
-// each x-run of cells one contiguous slot range (visited in slot order).  (Staging the
-// block's neighbourhood -- one contiguous slot range -- in LDS was measured 18 % slower
-// on config C: the walk is VALU-bound, and 64 KB of LDS halves the occupancy.)
+// each x-run of cells one contiguous slot range.  Measured on config C (kernel traces,
+// scripts/gpu_profab.sh): collecting the list in an LDS row and storing it a quad at a
+// time is 13 % faster than one global u16 store per entry; batches of 4 slots per run
+// beat 2 and 6.  Staging positions in LDS does not pay, neither the block's whole
+// neighbourhood range (~50 KB, 18 % slower) nor the union of the slots its lists use
+// (lists rewritten to union indices: this kernel +58 %, the force kernel +9 %).
 __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
-    int s, i;
-    if (!pop_build_slot(A, &s, &i)) return;
+    __shared__ uint32_t lrow[kPopBS * kPopListRow / 2];
+    const int kb = blockIdx.x / A.nbs;
+    if (kb >= *A.nflag) return;  // an idle block (the structure was not flagged)
+    const int s = A.flist[kb], blk = blockIdx.x % A.nbs, t = threadIdx.x, i = blk * kPopBS + t;
+    const bool live = i < A.cm.natom;
     const size_t base = (size_t)s * A.cm.ldn;
     const float4* pos = A.buf[A.par[s]].pos + base;
-    const float4 p0 = pos[i];
+    const float4 p0 = pos[live ? i : 0];
+    const bool bead = live && p0.w >= 0.0f;
     const float* gp = A.gp + (size_t)s * 8;
     const int* gn = A.gn + (size_t)s * 8;
     const int* cell = A.cell + (size_t)s * kPopCells;
-    const int kcap = A.cm.kcap;
-    uint16_t* out = A.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * kcap * 64 + (i & 63);
+    const int nx = gn[0], ny = gn[1], nz = gn[2];
+    const int kcap = 4 * A.kq;  // <= kPopListCap
+    // The list is collected in this thread's LDS row (one u16 store per entry), then
+    // copied out a quad at a time: entry k of the slot is u16 k & 3 of quad k >> 2, the
+    // quads of a slice's 64 slots interleaved (coalesced uint2 stores).
+    uint16_t* lst = reinterpret_cast<uint16_t*>(lrow) + t * kPopListRow;
     const float cut2 = A.P.cut_list * A.P.cut_list;
     int k = 0;
-    if (p0.w >= 0.0f) {
-        walk27(cell_index<float>(p0.x, p0.y, p0.z, gp, gp + 3, gn), cell, (const uint16_t*)nullptr, gn,
-               [&](int j, bool ok) {
-                   const float4 p = pos[j];
-                   const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
-                   const bool in = ok && j != i && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
-                   if (in && k < kcap) out[(size_t)k * 64] = (uint16_t)j;
-                   k += in ? 1 : 0;
-               });
+    if (bead) {
+        // The 27 cells are 9 x-runs of slots.  All 18 run bounds are loaded together,
+        // then each z-layer's 3 runs a batch of kFillW slots per run at once (the rare
+        // longer run finishes in a loop): 4 dependent memory round trips per slot in
+        // place of one per run and per batch.
+        const int c = cell_index<float>(p0.x, p0.y, p0.z, gp, gp + 3, gn);
+        const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+        const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
+        int rb[9], re[9];
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            const int z0 = cz + r / 3 - 1, y0 = cy + r % 3 - 1;
+            const bool ok = z0 >= 0 && z0 < nz && y0 >= 0 && y0 < ny;
+            const int row = ok ? (z0 * ny + y0) * nx : 0;
+            rb[r] = ok ? cell[row + xlo] : 0;
+            re[r] = ok ? cell[row + xhi + 1] : 0;
+        }
+        const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
+        auto test = [&](int j, const float3& p) {
+            const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
+            const bool in = j != i && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
+            if (in && k < kcap) lst[k] = (uint16_t)j;
+            k += in ? 1 : 0;
+        };
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            float3 pp[3][kFillW];
+            int jj[3][kFillW];
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int u = 0; u < kFillW; ++u) {
+                    const int j = rb[3 * g + r] + u;
+                    jj[r][u] = j < re[3 * g + r] ? j : i;  // past the run: the slot itself (never listed)
+                    pp[r][u] = pop_ld3(rp, jj[r][u]);
+                }
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+#pragma unroll
+                for (int u = 0; u < kFillW; ++u) test(jj[r][u], pp[r][u]);
+                for (int j = rb[3 * g + r] + kFillW; j < re[3 * g + r]; ++j) test(j, pop_ld3(rp, j));
+            }
+        }
+        // the last quad padded with the slot itself: a zero-distance entry adds no force
+        for (int kk = k; kk < kcap && (kk & 3); ++kk) lst[kk] = (uint16_t)i;
     }
-    A.nnb[base + i] = (uint16_t)(k <= kcap ? k : kNnbWalk);
+    const int nlist = bead && k <= kcap ? ((k + 3) & ~3) : 0;  // entries incl. the padding
+    if (nlist > 0) {
+        uint64_t* out = reinterpret_cast<uint64_t*>(A.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * A.kq * 64 + (i & 63));
+        const uint32_t* row = lrow + t * (kPopListRow / 2);
+#pragma unroll 1
+        for (int q = 0; q < nlist >> 2; ++q) out[(size_t)q * 64] = ((uint64_t)row[2 * q + 1] << 32) | row[2 * q];
+    }
+    if (live) A.nnb[base + i] = (uint16_t)(!bead ? 0 : (k <= kcap ? k : kNnbWalk));
 }
 
 // pair forces of a slot past the Verlet-list capacity: the 27 cells of the build-time
@@ -1313,24 +1439,39 @@ __device__ __noinline__ float4 pop_walk_pairs(const float4* pos, const int* cell
 __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, size_t base, const float4* pos,
                                                uint32_t fl, float evf, float envf, float& fx, float& fy,
                                                float& fz) {
-    constexpr int U = kPopPairBatch;
-    const int nsl = A.cm.nslice, amax = A.cm.natom - 1;
-    const uint16_t* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.cm.kcap * 64 + (i & 63);
+    constexpr int U = kPopPairBatch;  // list quads per batch
+    const int nsl = A.cm.nslice;
+    const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
     const uint32_t* g = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
+    const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
     const float4 p0 = pos[i];
     const float xi = p0.x, yi = p0.y, zi = p0.z, ri = p0.w;
     fx = fy = fz = 0.0f;
     const float evfpi = evf * 0.318309886183790671537767526745f;
     const int nn = A.nnb[base + i];
     const int deg = A.bdeg[base + i];
-    auto pair = [&](const float4& p, bool on) {
-        const float dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
-        const float f = soft_pair_bf(dx * dx + dy * dy + dz * dz, ri + p.w, evfpi);
-        const float m = on ? f : 0.0f;
-        fx += m * dx;
-        fy += m * dy;
-        fz += m * dz;
+    // Two list entries per packed-f32 op.  With t = 1/(r rc) from ONE rsq,
+    //   sin(pi r / rc) = sin_rev(r2 t / 2)   and   evf rc sin / (pi r) = evfpi rc2 t sin,
+    // the soft_pair_bf force without the rcp; the 1e-20 keeps a zero distance (the
+    // padding entries, which are the slot itself) finite, and it is below one ulp of
+    // every r2 that is not zero.
+    pop_f2 ax = {0.0f, 0.0f}, ay = {0.0f, 0.0f}, az = {0.0f, 0.0f};
+    auto pair2 = [&](const float4& a, const float4& b) {
+        const pop_f2 dx = pop_f2{xi, xi} - pop_f2{a.x, b.x}, dy = pop_f2{yi, yi} - pop_f2{a.y, b.y},
+                     dz = pop_f2{zi, zi} - pop_f2{a.z, b.z};
+        const pop_f2 r2 = dx * dx + dy * dy + dz * dz;
+        const pop_f2 rc = pop_f2{ri, ri} + pop_f2{a.w, b.w};
+        const pop_f2 rc2 = rc * rc;
+        const pop_f2 q = (r2 + 1.0e-20f) * rc2;
+        const pop_f2 t = {__builtin_amdgcn_rsqf(q.x), __builtin_amdgcn_rsqf(q.y)};
+        const pop_f2 h = (0.5f * r2) * t;
+        const pop_f2 sn = {__builtin_amdgcn_sinf(h.x), __builtin_amdgcn_sinf(h.y)};
+        const pop_f2 f = (evfpi * rc2) * (sn * t);
+        const pop_f2 m = {r2.x < rc2.x ? f.x : 0.0f, r2.y < rc2.y ? f.y : 0.0f};
+        ax += m * dx;
+        ay += m * dy;
+        az += m * dz;
     };
     auto bond = [&](const float4& p, float2 c, uint32_t e, bool on) {
         const float dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
@@ -1352,18 +1493,52 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
             fy = f.y;
             fz = f.z;
         } else {
-            for (int k0 = 0; k0 < nn; k0 += U) {
-                int jt[U];
+            const int nq = (nn + 3) >> 2;
+            auto pairs = [&](auto fetch) {
+                for (int q0 = 0; q0 < nq; q0 += U) {
+                    uint2 e[U];  // a quad past the list: the slot itself 4 times (no force)
 #pragma unroll
-                for (int u = 0; u < U; ++u) jt[u] = min((int)gl[(size_t)(k0 + u) * 64], amax);
-                float4 pt[U];
+                    for (int u = 0; u < U; ++u)
+                        e[u] = q0 + u < nq ? gl[(size_t)(q0 + u) * 64] : make_uint2(i * 0x10001u, i * 0x10001u);
+                    float4 pt[4 * U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) pt[u] = pos[jt[u]];
+                    for (int u = 0; u < U; ++u) {
+                        pt[4 * u + 0] = fetch(e[u].x & 0xffffu);
+                        pt[4 * u + 1] = fetch(e[u].x >> 16);
+                        pt[4 * u + 2] = fetch(e[u].y & 0xffffu);
+                        pt[4 * u + 3] = fetch(e[u].y >> 16);
+                    }
 #pragma unroll
-                for (int u = 0; u < U; ++u) pair(pt[u], k0 + u < nn);
+                    for (int u = 0; u < 2 * U; ++u) pair2(pt[2 * u], pt[2 * u + 1]);
+                }
+            };
+#ifdef IGM_POP_TIMING_PAIR_REPS  // timing variants only: the pair loop repeated, the repeats discarded
+            pop_f2 kx, ky, kz;
+            for (int rep = 0; rep < IGM_POP_TIMING_PAIR_REPS; ++rep) {
+#endif
+            pairs([&](uint32_t j) { return pop_ld(rp, j); });
+#ifdef IGM_POP_TIMING_PAIR_REPS
+                if (rep == 0) {
+                    kx = ax;
+                    ky = ay;
+                    kz = az;
+                }
             }
+            if (A.cm.natom >= 0) {
+                ax = kx;
+                ay = ky;
+                az = kz;
+            }
+#endif
+            fx = ax.x + ax.y;
+            fy = ay.x + ay.y;
+            fz = az.x + az.y;
         }
     }
+#ifdef IGM_POP_TIMING_BOND_REPS  // timing variants only: the bond loop repeated, the repeats discarded
+    float kfx = 0.0f, kfy = 0.0f, kfz = 0.0f;
+    for (int rep = 0; rep < IGM_POP_TIMING_BOND_REPS; ++rep) {
+#endif
     for (int k0 = 0; k0 < deg; k0 += 4) {
         uint32_t et[4];
 #pragma unroll
@@ -1372,12 +1547,25 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         float2 ct[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            pt[u] = pos[et[u] & 0xffffu];
+            pt[u] = pop_ld(rp, et[u] & 0xffffu);
             ct[u] = bt[(et[u] >> 16) & 0x7fffu];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) bond(pt[u], ct[u], et[u], k0 + u < deg);
     }
+#ifdef IGM_POP_TIMING_BOND_REPS
+        if (rep == 0) {
+            kfx = fx;
+            kfy = fy;
+            kfz = fz;
+        }
+    }
+    if (A.cm.natom >= 0) {
+        fx = kfx;
+        fy = kfy;
+        fz = kfz;
+    }
+#endif
     // envelopes (non-bead atoms carry -(radius + 1))
     const float rad = ri >= 0.0f ? ri : -ri - 1.0f;
     for (int e = 0; e < A.P.nenv; ++e) {
@@ -1410,7 +1598,9 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 }
 
 // forces of every slot (+ final_integrate and this block's kinetic-energy partial
-// when S.integrate; the run's setup evaluation otherwise)
+// when S.integrate; the run's setup evaluation otherwise).  (Measured on config C: a
+// block running the pairs and the bonds of its slots in separate waves at the same
+// time is 6 % slower than one thread per slot doing both.)
 __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(PopArgs A, float evf, float envf, PopStep S) {
     __shared__ double red[kPopBS / 64];
     const int lb = pop_block(), s = lb / A.nbs, blk = lb % A.nbs, i = blk * kPopBS + threadIdx.x;
@@ -2455,7 +2645,7 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
         V.buf[b] = PopBuf{Q.buf[b].pos + o, Q.buf[b].vel + o, Q.buf[b].frc + o, Q.buf[b].aid + o, Q.buf[b].slot + o};
     V.par = Q.par + s0;
     V.xb = Q.xb + o;
-    V.nl = Q.nl + (size_t)s0 * nsl * Q.cm.kcap * 64;
+    V.nl = Q.nl + (size_t)s0 * nsl * Q.kq * 64;
     V.nnb = Q.nnb + o;
     V.cell = Q.cell + (size_t)s0 * kPopCells;
     V.gp = Q.gp + (size_t)s0 * 8;
@@ -2506,8 +2696,8 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     void *ppar, *pxb, *pnl, *pnnb, *pcell, *pgp, *pgn, *pbent, *pbdeg, *pfl, *pfli, *pnf, *pke, *pbb;
     IGM_TRY(workspace(c, "pop_par", sizeof(int) * S, &ppar));
     IGM_TRY(workspace(c, "pop_xb", sizeof(float4) * SL, &pxb));
-    // + slack: the batched force loop reads up to kPopPairBatch - 1 slots past a list
-    IGM_TRY(workspace(c, "pop_nl", sizeof(uint16_t) * (SL * pr.cm.kcap + 64 * kPopPairBatch), &pnl));
+    Q.kq = (std::min(pr.cm.kcap, kPopListCap) + 3) / 4;
+    IGM_TRY(workspace(c, "pop_nl", sizeof(uint2) * SL * Q.kq, &pnl));
     IGM_TRY(workspace(c, "pop_nnb", sizeof(uint16_t) * SL, &pnnb));
     IGM_TRY(workspace(c, "pop_cell", sizeof(int) * (size_t)S * kPopCells, &pcell));
     IGM_TRY(workspace(c, "pop_gp", sizeof(float) * 8 * (size_t)S, &pgp));
@@ -2523,7 +2713,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     if (!pnr) IGM_TRY(workspace(c, "pop_nreb", sizeof(int) * (size_t)S, &pnr));
     Q.par = (int*)ppar;
     Q.xb = (float4*)pxb;
-    Q.nl = (uint16_t*)pnl;
+    Q.nl = (uint2*)pnl;
     Q.nnb = (uint16_t*)pnnb;
     Q.cell = (int*)pcell;
     Q.gp = (float*)pgp;
@@ -2560,7 +2750,9 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     // the sort keeps its ids in LDS when they fit beside the cell counts (200 kb: 29 839 atoms)
     const bool ids_lds = pop_sort_lds(true, N) <= kLdsBytes;
     const size_t sort_lds = pop_sort_lds(ids_lds, N);
-    auto sort_kern = ids_lds ? pop_sort_kernel<true> : pop_sort_kernel<false>;
+    auto sort_kern = !ids_lds ? pop_sort_kernel<false, 0>
+                     : N <= 16 * kPopSortNT ? pop_sort_kernel<true, 16>
+                     : N <= 32 * kPopSortNT ? pop_sort_kernel<true, 32> : pop_sort_kernel<true, 0>;
     IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)sort_kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)sort_lds));
     // Structure groups on auxiliary streams: while one group waits in its latency-bound
@@ -2942,14 +3134,16 @@ extern "C" int igm_velocity_create(igm_ctx* c, uint32_t flags, int32_t nseed, in
     return finish(c, flags);
 }
 
-/* Profiling aid (IGM_PROF=1 in the environment): cycle counters of the last LDS-path
- * anneal launch summed over structures: {build, force, rest, steps, builds}. */
+/* Volumetric envelopes: stage the EDT maps (and the structure -> map table) that
+ * IGM_ENV_VOLUME envelopes of the next runs read. */
 extern "C" int igm_mstep_set_volumes(igm_ctx* c, int32_t nmap, const igm_volume_map* maps,
                                      const int32_t* struct_map, int32_t nstruct) {
     if (!c) return IGM_E_INVALID;
     return set_volumes(c, nmap, maps, struct_map, nstruct);
 }
 
+/* Profiling aid (IGM_PROF=1 in the environment): cycle counters of the last LDS-path
+ * anneal launch summed over structures: {build, force, rest, steps, builds}. */
 extern "C" int igm_mstep_last_profile(igm_ctx* c, unsigned long long* out) {
     if (!c || !out) return IGM_E_INVALID;
     auto it = c->ws.find("ms_prof");

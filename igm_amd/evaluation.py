@@ -17,7 +17,11 @@ buildContactMap and sumCopies live in alabtools, which is not in the reference t
 nor importable here: the contact test restated is IGM's own Hi-C contact (float32 norm
 of inter_hic.py:47 against the HarmonicUpperBound r0 of restraints/hic.py), and the copy
 sum is the plain sum over copy pairs.  Parity of those two is unpinned; the score
-arithmetic follows HicEvaluationStep.reduce line by line.
+arithmetic follows HicEvaluationStep.reduce line by line.  The comparison is '<=' (a
+contact is a satisfied HarmonicUpperBound, inter_hic.py); the commented-out task of
+HicEvaluationStep.py:89-91 writes a strict '<'.  The two differ only for a distance
+exactly equal to the bound (test_evaluation.py's near-tie case pins which side each
+split decision falls on).
 """
 import numpy as np
 

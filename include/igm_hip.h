@@ -169,7 +169,9 @@ int igm_polymer_assign(igm_ctx* ctx, uint32_t flags,
  * (igm/steps/HicEvaluationStep.py:96-179) builds with HssFile.buildContactMap
  * (contactRange) at :109 (alabtools, absent here: the contact test restated is the
  * IGM Hi-C one, |x_i - x_j| (float32 norm, inter_hic.py:47) <= fl32(contact_range *
- * fl32(r_i + r_j))).  counts (nbead, nbead) int32, symmetric, diagonal included, =
+ * fl32(r_i + r_j))); the commented-out task of HicEvaluationStep.py:89-91 uses a
+ * strict '<', which differs only for a distance exactly at the bound).
+ * counts (nbead, nbead) int32, symmetric, diagonal included, =
  * the number of structures in contact; the caller divides by nstruct and sums the
  * copies (Contactmatrix.sumCopies, :111-112). */
 int igm_contact_map(igm_ctx* ctx, uint32_t flags,

@@ -15,11 +15,11 @@ while read -r CNT; do
   i=$((i+1))
   timeout -s KILL 300 rocprofv3 --pmc $CNT -d $OUT/p$i -o p$i -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i ($CNT) rc=$rc"; [ $rc -eq 0 ] || exit $rc
-done <<'L'
-FETCH_SIZE
+done <<L
+${PASSES:-FETCH_SIZE
 WRITE_SIZE
 TCC_HIT_sum TCC_MISS_sum
-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU
+SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU}
 L
 python3 scripts/pmc_show.py $OUT pop_ > $OUT/pmc_pop.txt 2>&1
 python3 scripts/pmc_show.py $OUT cg_kernel > $OUT/pmc_cg.txt 2>&1

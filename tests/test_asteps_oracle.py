@@ -1,5 +1,8 @@
 """CPU: the configuration D/E A-step oracle (oracle/asteps.py) against the golden
 vectors of the reference functions (tests/golden/make_golden_asteps.py)."""
+import ctypes
+import os
+
 import numpy as np
 import pytest
 
@@ -89,6 +92,36 @@ def test_sprite_get_rgs2_known_answers():
                 v = A.rg2_f32([alts[i][comb[i]] for i in range(len(alts))])
                 best = min(best, v) if v < best else best
             assert best == g['kat%d_rg2s' % q][s]
+
+
+REF_SPRITE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'oracle', '_ref',
+                          'libsprite_ref.so')
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SPRITE), reason='oracle/_ref not built (make -C oracle ref)')
+def test_compiled_reference_sprite_kernel_reproduces_goldens(pop):
+    """oracle/_ref/libsprite_ref.so -- the reference's cpp_sprite_assignment.cpp compiled
+    from /root/reference by oracle/Makefile -- against the goldens its Cython build wrote
+    (make_golden.py:450-489): the demo cases and the known-answer cases, bit for bit."""
+    lib = ctypes.CDLL(REF_SPRITE)
+    g = load_golden('sprite_golden.npz')
+    P = np.ctypeslib.ndpointer
+    lib.sprite_ref_get_rg2s.argtypes = [P(np.float32, flags='C'), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        P(np.int32, flags='C'), P(np.float32, flags='C'), P(np.int32, flags='C'),
+                                        ctypes.POINTER(ctypes.c_int)]
+    cases = [('s%d' % c, pop['coordinates'][g['s%d_beads' % c]]) for c in range(int(g['ncases']))]
+    cases += [('kat%d' % q, g['kat%d_crd' % q]) for q in range(int(g['nkat']))]
+    for tag, crd in cases:
+        crd = np.ascontiguousarray(crd, np.float32)
+        cn = np.ascontiguousarray(g[tag + '_ncopies'], np.int32)
+        S = crd.shape[1]
+        rg2s = np.zeros(S, np.float32)
+        cidx = np.zeros((S, len(cn)), np.int32)
+        best = ctypes.c_int(-1)
+        lib.sprite_ref_get_rg2s(crd, S, crd.shape[0], len(cn), cn, rg2s, cidx, ctypes.byref(best))
+        assert np.array_equal(rg2s.view(np.uint32), g[tag + '_rg2s'].view(np.uint32)), tag
+        assert np.array_equal(cidx, g[tag + '_copy_idxs']), tag
+        assert best.value == int(g[tag + '_best']), tag
 
 
 def exp_maps(g):
