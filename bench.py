@@ -392,7 +392,9 @@ def main():
                            ' x%g (NOT the metric)' % args.protocol_scale),
                        'nstruct_per_gpu': it.S_local, 'nstruct_total': total, 'sigma': args.sigma,
                        'npairs': int(it.npairs_total), 'parallelism': 'structures sharded, A-step pair-sharded'},
-            'roofline': {'bound': 'hbm', 'kernel': 'anneal_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+            'roofline': {'bound': 'hbm', 'kernel': 'anneal_kernel' if args.config == 'B' else
+                         'population engine (pop_integrate, pop_sort, pop_permute, pop_fill, pop_force per MD step)',
+                         'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'traffic_source': traffic_src,
                          'algorithmic_bytes_per_launch': float(np.mean(bytes_launch)),

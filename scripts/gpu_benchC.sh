@@ -13,7 +13,12 @@ if [ -n "$PRE" ]; then
   rc=$?; tail -3 $OUT/pre_tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 (nproc; lscpu | grep -i "model name"; rocm-smi --showproductname 2>/dev/null | head -20) > $OUT/host.txt 2>&1
-timeout -k 10 900 python -u bench.py --config C --steps 1 --warmup 1 --cpu-sample 16 --no-de > $OUT/bench.log 2>&1
+# a heartbeat under gpurun_out/ while the long, silent runs go (killed by its PID at exit)
+(while sleep 50; do date >> $OUT/heartbeat.txt; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+# (no CPU sample here: the config C CPU baseline is the scaled one of the default bench line)
+timeout -k 10 900 python -u bench.py --config C --steps 1 --warmup 1 --cpu-sample 0 --no-de > $OUT/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep "^{" $OUT/bench.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
 PARGS="--config C --steps 1 --warmup 1 --cpu-sample 0 --no-de"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt -- python3 bench.py $PARGS > $OUT/prof_kt.log 2>&1
