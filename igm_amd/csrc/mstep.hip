@@ -905,7 +905,10 @@ constexpr int kPopCells = kCellCapBig + 2;  // cell offsets of a structure: real
 #define IGM_POP_FILL_W 4
 #endif
 constexpr int kFillW = IGM_POP_FILL_W;  // list build: slots per x-run loaded in one batch
-constexpr int kPopListCap = 64;          // Verlet-list entries per slot (more: the cell walk)
+#ifndef IGM_POP_LIST_CAP
+#define IGM_POP_LIST_CAP 64
+#endif
+constexpr int kPopListCap = IGM_POP_LIST_CAP;  // Verlet-list entries per slot (more: the cell walk)
 constexpr int kPopListRow = kPopListCap + 2;  // u16 per LDS list row of the build (odd word stride)
 
 struct PopBuf {
