@@ -906,7 +906,7 @@ constexpr int kPopCells = kCellCapBig + 2;  // cell offsets of a structure: real
 #endif
 constexpr int kFillW = IGM_POP_FILL_W;  // list build: slots per x-run loaded in one batch
 #ifndef IGM_POP_LIST_CAP
-#define IGM_POP_LIST_CAP 64
+#define IGM_POP_LIST_CAP 48  // measured on config C: 48 beats 64 (fill occupancy) and 40 (more cell walks)
 #endif
 constexpr int kPopListCap = IGM_POP_LIST_CAP;  // Verlet-list entries per slot (more: the cell walk)
 constexpr int kPopListRow = kPopListCap + 2;  // u16 per LDS list row of the build (odd word stride)
@@ -1020,16 +1020,20 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     __shared__ float red[kPopBS / 64 * 6];
     const int lb = pop_block(), s = lb / A.nbs, i = (lb % A.nbs) * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
-    const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
     const PopBuf& B = A.buf[A.par[s]];
+    // the slot's state is loaded before the rescale factor's block reduction, so the
+    // loads are in flight while wave 0 sums the KE partials
+    const bool live = i < A.cm.natom;
+    const size_t k = (size_t)s * A.cm.ldn + (live ? i : 0);
+    float4 p = B.pos[k];
+    float4 v = B.vel[k];
+    const float4 f = B.frc[k];
+    const float4 b = A.xb[k];
+    const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
     int moved = 0;
     float mm[6] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
-    if (i < A.cm.natom) {
-        const size_t k = (size_t)s * A.cm.ldn + i;
-        float4 p = B.pos[k];
-        float4 v = B.vel[k];
+    if (live) {
         if (S.integrate && !(__float_as_uint(v.w) & IGM_ATOM_FIXED)) {
-            const float4 f = B.frc[k];
             v.x *= factor;
             v.y *= factor;
             v.z *= factor;
@@ -1041,7 +1045,6 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
             B.pos[k] = p;
         }
         if (p.w >= 0.0f) {
-            const float4 b = A.xb[k];
             const float dx = p.x - b.x, dy = p.y - b.y, dz = p.z - b.z;
             moved = !(dx * dx + dy * dy + dz * dz <= S.trig);
             mm[0] = -p.x;
@@ -1214,15 +1217,19 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A) {
     };
     auto get = [&](int k) -> int { return IDS_LDS ? (int)ids[k] : aidn[k]; };
     if constexpr (APT > 0) {
-        int aa[APT];
 #pragma unroll
-        for (int u = 0; u < APT; ++u) {
-            const int i = t + u * kPopSortNT;
-            aa[u] = aido[i < N ? i : 0];
+        for (int u0 = 0; u0 < APT; u0 += 16) {
+            int aa[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int i = t + (u0 + u) * kPopSortNT;
+                aa[u] = aido[i < N ? i : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (u0 + u < APT && t + (u0 + u) * kPopSortNT < N)
+                    put(off((int)(cr[u0 + u] >> 16)) + (int)(cr[u0 + u] & 0xffffu), aa[u]);
         }
-#pragma unroll
-        for (int u = 0; u < APT; ++u)
-            if (t + u * kPopSortNT < N) put(off((int)(cr[u] >> 16)) + (int)(cr[u] & 0xffffu), aa[u]);
     } else
     for (int i0 = t; i0 < N; i0 += U * kPopSortNT) {
         uint32_t uu[U];
@@ -1238,23 +1245,39 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A) {
             if (i0 + u * kPopSortNT < N) put(off((int)(uu[u] >> 16)) + (int)(uu[u] & 0xffffu), aa[u]);
     }
     __syncthreads();
-    for (int c = t; c <= ncell; c += kPopSortNT) {  // deterministic order inside a cell
-        const int beg = off(c), end = off(c + 1);
-        for (int i = beg + 1; i < end; ++i) {
-            const int v = get(i);
-            int k = i - 1;
-            while (k >= beg && get(k) > v) {
-                put(k + 1, get(k));
-                --k;
-            }
-            put(k + 1, v);
+    if constexpr (APT > 0) {
+        // deterministic order inside a cell: an atom's slot is its cell's first slot plus
+        // the number of the cell's atoms with a smaller id (independent LDS reads per
+        // atom, where an insertion sort per cell is a serial chain of them)
+#pragma unroll
+        for (int u = 0; u < APT; ++u) {
+            if (t + u * kPopSortNT >= N) continue;
+            const int c = (int)(cr[u] >> 16), beg = off(c), end = off(c + 1);
+            const int a = get(beg + (int)(cr[u] & 0xffffu));
+            int r = 0;
+            for (int k = beg; k < end; ++k) r += get(k) < a ? 1 : 0;
+            aidn[beg + r] = a;
+            slotn[a] = beg + r;
         }
-    }
-    __syncthreads();
-    for (int i = t; i < N; i += kPopSortNT) {
-        const int a = get(i);
-        if (IDS_LDS) aidn[i] = a;
-        slotn[a] = i;
+    } else {
+        for (int c = t; c <= ncell; c += kPopSortNT) {  // deterministic order inside a cell
+            const int beg = off(c), end = off(c + 1);
+            for (int i = beg + 1; i < end; ++i) {
+                const int v = get(i);
+                int k = i - 1;
+                while (k >= beg && get(k) > v) {
+                    put(k + 1, get(k));
+                    --k;
+                }
+                put(k + 1, v);
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < N; i += kPopSortNT) {
+            const int a = get(i);
+            if (IDS_LDS) aidn[i] = a;
+            slotn[a] = i;
+        }
     }
     int* cg = A.cell + (size_t)s * kPopCells;
     for (int c = t; c <= ncell + 1; c += kPopSortNT) cg[c] = off(c);
