@@ -99,7 +99,7 @@ struct BondView {
     const uint32_t* g;
     const float2* gt;
     const uint16_t* l;
-    const float2* lt;
+    const float4* lt;  // LDS bond types {r0^2, 2 k r0, -2 k, k}
     int n;
 };
 
@@ -169,7 +169,7 @@ struct MdLds {
     Red r;
     float4* pos;
     uint16_t* boff;  // npad+8 bond CSR offsets
-    float2* btab;    // kLdsBondTypes (r0, k)
+    float4* btab;    // kLdsBondTypes {r0^2, 2 k r0, -2 k, k}
     uint16_t* rest;  // the structure's bond CSR, when it fits
     int rest_cap;    // u16 entries
     NList<float, uint16_t> L;
@@ -184,7 +184,7 @@ __host__ __device__ inline MdLds carve_md_lds(void* smem, int npad) {
     m.L.nnb = cv.take<uint16_t>(npad);
     m.L.sorted = cv.take<uint16_t>(npad);
     m.boff = cv.take<uint16_t>(npad + 8);
-    m.btab = cv.take<float2>(kLdsBondTypes);
+    m.btab = cv.take<float4>(kLdsBondTypes);
     m.L.lell = cv.take<uint16_t>((size_t)kLdsListSlots * npad);
     m.L.lstride = npad;
     m.L.kl = kLdsListSlots;
@@ -469,120 +469,36 @@ __device__ __noinline__ void pair_walk(int a, T xi, T yi, T zi, T ri, const vec4
     if (EN) ep += e;
 }
 
-// Total force on atom a, gathered by its owner thread: pairs from the Verlet
-// list (or the cell walk around the build-time position b*), bonds B, envelopes.
-template <typename T, bool EN, typename OffT, int PB = IGM_PAIR_BATCH>
-__device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, uint32_t fl, const vec4_t<T>* pos,
-                                           const NList<T, OffT>& L, T bx, T by, T bz, const BondView& B,
-                                           const DevParams& P, T evf, T envf, T& fx, T& fy,
-                                           T& fz, double& ep, double& eb, double (&ee)[IGM_MAX_ENVELOPES]) {
-    fx = fy = fz = T(0);
-    const T xi = p0.x, yi = p0.y, zi = p0.z;
-    const T ri = (T)p0.w;
-    if (ri >= T(0)) {
-        const int nn = L.nnb[a];
-        if (nn == kNnbWalk) {
-            pair_walk<T, EN, OffT>(a, xi, yi, zi, ri, pos, L, bx, by, bz, P, evf, fx, fy, fz, ep);
-        } else if (nn > 0) {
-            // the LDS slots, then the HBM slots, in batches whose loads are all in flight together
-            constexpr int U = PB;  // neighbours whose loads are in flight together
-            const int n1 = nn < L.kl ? nn : L.kl;
-            const uint16_t* gl = L.gell + (size_t)(a >> 6) * L.kg * 64 + (a & 63);
-            if constexpr (std::is_same<T, float>::value) {
-                // one batch of U neighbours of a slot sequence idx(k), k < n (tail masked)
-                // slots k0..k0+U-1 are always readable (LDS: kl is a multiple of U; HBM:
-                // the overflow regions carry U-1 slack slots); a slot past n holds a stale
-                // or scratch value, clamped to a valid atom and masked out.  Keeping the
-                // slot offset wave-uniform turns the address arithmetic scalar.
-                const int amax = P.natom - 1;
-                const float evfpi = evf * 0.318309886183790671537767526745f;
-                auto batch = [&](int k0, int n, auto idx) {
-                    int jv[U];
+// the bonds of one atom from the HBM adjacency (B.g, B.gt; B.n entries)
+template <typename T, bool EN>
+__device__ __forceinline__ void hbm_bonds(T xi, T yi, T zi, const vec4_t<T>* pos, const BondView& B, T& fx, T& fy,
+                                          T& fz, double& eb) {
+    constexpr int UB = 4;  // HBM bond entries per batch
+    for (int k0 = 0; k0 < B.n; k0 += UB) {
+        uint32_t ev[UB];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) jv[u] = min((int)idx(k0 + u), amax);
-                    float4 pj[U];
+        for (int u = 0; u < UB; ++u) ev[u] = (k0 + u < B.n) ? B.g[(size_t)(k0 + u) * 64] : 0u;
 #pragma unroll
-                    for (int u = 0; u < U; ++u) pj[u] = pos[jv[u]];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const float dx = xi - pj[u].x, dy = yi - pj[u].y, dz = zi - pj[u].z;
-                        const float fp = soft_pair_bf(dx * dx + dy * dy + dz * dz, ri + pj[u].w, evfpi);
-                        const float m = (k0 + u < n) ? fp : 0.0f;
-                        fx += m * dx;
-                        fy += m * dy;
-                        fz += m * dz;
-                    }
-                };
-                const uint16_t* ll = L.lell + a;
-                const int ls = __builtin_amdgcn_readfirstlane(L.lstride);  // uniform: scalar slot offsets
-                for (int k0 = 0; k0 < n1; k0 += U) batch(k0, n1, [&](int k) { return ll[(size_t)k * ls]; });
-                const int n2 = nn - n1;
-                for (int k0 = 0; k0 < n2; k0 += U) batch(k0, n2, [&](int k) { return gl[(size_t)k * 64]; });
-            } else {
-                for (int k0 = 0; k0 < nn; k0 += U) {
-                    int jv[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const int k = k0 + u;
-                        jv[u] = k >= nn ? -1 : (k < n1 ? (int)L.lell[(size_t)k * L.lstride + a] : (int)gl[(size_t)(k - n1) * 64]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        if (jv[u] >= 0) pair_one<T, EN>(jv[u], xi, yi, zi, ri, pos, P, evf, fx, fy, fz, ep);
-                }
-            }
+        for (int u = 0; u < UB; ++u) {
+            if (k0 + u >= B.n) continue;
+            const uint32_t e32 = ev[u];
+            const float2 rk = B.gt[(e32 >> 16) & 0x7fffu];
+            const vec4_t<T> p = pos[e32 & 0xffffu];
+            const T dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
+            double e = 0.0;
+            const T fb = bond_term<T, EN>(dx * dx + dy * dy + dz * dz, (T)rk.x, (T)rk.y, (e32 & kLowerBit) != 0u, e);
+            fx += fb * dx;
+            fy += fb * dy;
+            fz += fb * dz;
+            if (EN) eb += 0.5 * e;
         }
     }
-    if (B.l && B.n > 0) {
-        constexpr int UL = IGM_BOND_BATCH;  // LDS bond entries per batch, branch-free
-        for (int k0 = 0; k0 < B.n; k0 += UL) {
-            uint32_t ev[UL];
-#pragma unroll
-            for (int u = 0; u < UL; ++u) ev[u] = (uint32_t)B.l[k0 + u < B.n ? k0 + u : B.n - 1];
-            float2 rk[UL];
-            vec4_t<T> pj[UL];
-#pragma unroll
-            for (int u = 0; u < UL; ++u) {
-                rk[u] = B.lt[ev[u] >> 13];
-                pj[u] = pos[ev[u] & 0xfffu];
-            }
-#pragma unroll
-            for (int u = 0; u < UL; ++u) {
-                const T dx = xi - pj[u].x, dy = yi - pj[u].y, dz = zi - pj[u].z;
-                double e = 0.0;
-                const T fb = bond_term_bf<T, EN>(dx * dx + dy * dy + dz * dz, (T)rk[u].x, (T)rk[u].y,
-                                                 ((ev[u] >> 12) & 1u) != 0u, e);
-                const T m = (k0 + u < B.n) ? fb : T(0);
-                fx += m * dx;
-                fy += m * dy;
-                fz += m * dz;
-                if (EN && k0 + u < B.n) eb += 0.5 * e;
-            }
-        }
-    } else if (B.l) {
-    } else {
-        constexpr int UB = 4;  // HBM bond entries per batch
-        for (int k0 = 0; k0 < B.n; k0 += UB) {
-            uint32_t ev[UB];
-#pragma unroll
-            for (int u = 0; u < UB; ++u) ev[u] = (k0 + u < B.n) ? B.g[(size_t)(k0 + u) * 64] : 0u;
-#pragma unroll
-            for (int u = 0; u < UB; ++u) {
-                if (k0 + u >= B.n) continue;
-                const uint32_t e32 = ev[u];
-                const float2 rk = B.gt[(e32 >> 16) & 0x7fffu];
-                const vec4_t<T> p = pos[e32 & 0xffffu];
-                const T dx = xi - p.x, dy = yi - p.y, dz = zi - p.z;
-                double e = 0.0;
-                const T fb =
-                    bond_term<T, EN>(dx * dx + dy * dy + dz * dz, (T)rk.x, (T)rk.y, (e32 & kLowerBit) != 0u, e);
-                fx += fb * dx;
-                fy += fb * dy;
-                fz += fb * dz;
-                if (EN) eb += 0.5 * e;
-            }
-        }
-    }
+}
+
+// envelope terms and fix setforce of one atom (radius/type ri as stored in pos.w)
+template <typename T, bool EN>
+__device__ __forceinline__ void env_terms(int s, T xi, T yi, T zi, T ri, uint32_t fl, const DevParams& P, T envf,
+                                          T& fx, T& fy, T& fz, double (&ee)[IGM_MAX_ENVELOPES]) {
     // non-bead atoms carry -(w + 1); f32: w = radius, f64: w = atom type
     T rad;
     if constexpr (std::is_same<T, float>::value)
@@ -604,6 +520,165 @@ __device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, ui
         if (EN) ee[e] += en;
     }
     if (fl & IGM_ATOM_FIXED) fx = fy = fz = T(0);  // fix setforce 0 (lammps.py:222-223)
+}
+
+// Total force on atom a, gathered by its owner thread: pairs from the Verlet
+// list (or the cell walk around the build-time position b*), bonds B, envelopes
+// (the CG kernel; the f32 MD kernel uses atom_force_md).
+template <typename T, bool EN, typename OffT, int PB = IGM_PAIR_BATCH>
+__device__ __forceinline__ void atom_force(int s, int a, const vec4_t<T>& p0, uint32_t fl, const vec4_t<T>* pos,
+                                           const NList<T, OffT>& L, T bx, T by, T bz, const BondView& B,
+                                           const DevParams& P, T evf, T envf, T& fx, T& fy,
+                                           T& fz, double& ep, double& eb, double (&ee)[IGM_MAX_ENVELOPES]) {
+    fx = fy = fz = T(0);
+    const T xi = p0.x, yi = p0.y, zi = p0.z;
+    const T ri = (T)p0.w;
+    if (ri >= T(0)) {
+        const int nn = L.nnb[a];
+        if (nn == kNnbWalk) {
+            pair_walk<T, EN, OffT>(a, xi, yi, zi, ri, pos, L, bx, by, bz, P, evf, fx, fy, fz, ep);
+        } else if (nn > 0) {
+            constexpr int U = PB;  // neighbours whose loads are in flight together
+            const int n1 = nn < L.kl ? nn : L.kl;
+            const uint16_t* gl = L.gell + (size_t)(a >> 6) * L.kg * 64 + (a & 63);
+            for (int k0 = 0; k0 < nn; k0 += U) {
+                int jv[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = k0 + u;
+                    jv[u] = k >= nn ? -1 : (k < n1 ? (int)L.lell[(size_t)k * L.lstride + a] : (int)gl[(size_t)(k - n1) * 64]);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (jv[u] >= 0) pair_one<T, EN>(jv[u], xi, yi, zi, ri, pos, P, evf, fx, fy, fz, ep);
+            }
+        }
+    }
+    hbm_bonds<T, EN>(xi, yi, zi, pos, B, fx, fy, fz, eb);
+    env_terms<T, EN>(s, xi, yi, zi, ri, fl, P, envf, fx, fy, fz, ee);
+}
+
+// soft-pair f/r of one flagged pair, without the evf/pi factor (applied once per
+// atom): ONE v_rsq, t = 1/(r rc): sin(pi r/rc) = sin_rev(r^2 t / 2),
+// f/r = evf/pi rc sin / r = evf/pi * rc^2 t sin.  Coincident atoms: 0.
+__device__ __forceinline__ float soft_pair_t(float r2, float rc) {
+    const float rc2 = rc * rc;
+    const float t = __builtin_amdgcn_rsqf(fmaxf(r2 * rc2, 1.0e-30f));
+    const float s = __builtin_amdgcn_sinf(0.5f * (r2 * t));
+    return r2 > 0.0f ? rc2 * t * s : 0.0f;
+}
+
+// f32 MD force of atom a in the LDS anneal kernel.  Pairs in two passes over
+// the Verlet list: a distance filter over every entry (one bit per entry inside
+// r_i + r_j) and the soft-pair force of the flagged entries only.  In a relaxed
+// structure ~2% of the list interacts (the list reaches cut_list = rc_max + skin),
+// so the rsq/sin work runs once or twice per atom instead of once per entry, and
+// the filter pass is a gather, 6 FMA-class ops and a compare.  Entries are
+// visited in slot order in both passes (fixed summation order).  LDS bonds take
+// one rsq each from the type table {r0^2, 2 k r0, -2 k}: f/r = 2 k r0/r - 2 k.
+template <int U>
+__device__ __forceinline__ void atom_force_md(int s, int a, const float4& p0, uint32_t fl, const float4* pos,
+                                              const NList<float, uint16_t>& L, float bx, float by, float bz,
+                                              const BondView& B, const DevParams& P, float evf,
+                                              float envf, float& fx, float& fy, float& fz) {
+    fx = fy = fz = 0.0f;
+    const float xi = p0.x, yi = p0.y, zi = p0.z, ri = p0.w;
+    double unused = 0.0;
+    if (ri >= 0.0f) {
+        const int nn = L.nnb[a];
+        if (nn == kNnbWalk) {
+            pair_walk<float, false, uint16_t>(a, xi, yi, zi, ri, pos, L, bx, by, bz, P, evf, fx, fy, fz, unused);
+        } else if (nn > 0) {
+            // slots k0..k0+U-1 are always readable (LDS: kl is a multiple of U; HBM: the
+            // overflow regions carry U-1 slack slots); a slot past n holds a stale or
+            // scratch value, clamped to a valid atom, its bit cleared after the pass
+            const int amax = P.natom - 1;
+            const int n1 = nn < L.kl ? nn : L.kl;
+            const uint16_t* ll = L.lell + a;
+            const int ls = __builtin_amdgcn_readfirstlane(L.lstride);  // uniform: scalar slot offsets
+            const uint16_t* gl = L.gell + (size_t)(a >> 6) * L.kg * 64 + (a & 63);
+            float gx = 0.0f, gy = 0.0f, gz = 0.0f;
+            auto filter = [&](int k0, int n, auto idx) {  // bits of the entries k0 .. k0+31 inside r_i + r_j
+                uint32_t m = 0u;
+                for (int k = 0; k < 32 && k0 + k < n; k += U) {
+                    int jv[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) jv[u] = min((int)idx(k0 + k + u), amax);
+                    float4 pj[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) pj[u] = pos[jv[u]];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const float dx = xi - pj[u].x, dy = yi - pj[u].y, dz = zi - pj[u].z;
+                        const float rc = ri + pj[u].w;
+                        m |= (dx * dx + dy * dy + dz * dz < rc * rc) ? (1u << (k + u)) : 0u;
+                    }
+                }
+                const int left = n - k0;
+                return left >= 32 ? m : m & ((1u << left) - 1u);
+            };
+            auto force = [&](int j) {
+                const float4 pj = pos[j];
+                const float dx = xi - pj.x, dy = yi - pj.y, dz = zi - pj.z;
+                const float f = soft_pair_t(dx * dx + dy * dy + dz * dz, ri + pj.w);
+                gx += f * dx;
+                gy += f * dy;
+                gz += f * dz;
+            };
+            {
+                uint32_t m = filter(0, n1, [&](int k) { return ll[(size_t)k * ls]; });  // kl <= 32
+                while (m) {
+                    const int k = __builtin_ctz(m);
+                    m &= m - 1u;
+                    force(ll[(size_t)k * ls]);
+                }
+            }
+            const int n2 = nn - n1;
+            for (int w0 = 0; w0 < n2; w0 += 32) {
+                uint32_t m = filter(w0, n2, [&](int k) { return gl[(size_t)k * 64]; });
+                while (m) {
+                    const int k = __builtin_ctz(m);
+                    m &= m - 1u;
+                    force(gl[(size_t)(w0 + k) * 64]);
+                }
+            }
+            const float evfpi = evf * 0.318309886183790671537767526745f;
+            fx = evfpi * gx;
+            fy = evfpi * gy;
+            fz = evfpi * gz;
+        }
+    }
+    if (B.l) {
+        constexpr int UL = IGM_BOND_BATCH;  // LDS bond entries per batch, branch-free
+        for (int k0 = 0; k0 < B.n; k0 += UL) {
+            uint32_t ev[UL];
+#pragma unroll
+            for (int u = 0; u < UL; ++u) ev[u] = (uint32_t)B.l[k0 + u < B.n ? k0 + u : B.n - 1];
+            float4 q[UL];
+            float4 pj[UL];
+#pragma unroll
+            for (int u = 0; u < UL; ++u) {
+                q[u] = B.lt[ev[u] >> 13];
+                pj[u] = pos[ev[u] & 0xfffu];
+            }
+#pragma unroll
+            for (int u = 0; u < UL; ++u) {
+                const float dx = xi - pj[u].x, dy = yi - pj[u].y, dz = zi - pj[u].z;
+                const float r2 = dx * dx + dy * dy + dz * dz;
+                // upper bound active beyond r0, lower bound inside it
+                const bool act = (r2 > q[u].x) != (((ev[u] >> 12) & 1u) != 0u);
+                const float fb = q[u].y * __builtin_amdgcn_rsqf(fmaxf(r2, 1.0e-30f)) + q[u].z;
+                const float m = (act && k0 + u < B.n) ? fb : 0.0f;
+                fx += m * dx;
+                fy += m * dy;
+                fz += m * dz;
+            }
+        }
+    } else {
+        hbm_bonds<float, false>(xi, yi, zi, pos, B, fx, fy, fz, unused);
+    }
+    double ee[IGM_MAX_ENVELOPES];
+    env_terms<float, false>(s, xi, yi, zi, ri, fl, P, envf, fx, fy, fz, ee);
 }
 
 // ------------------------------------------------------------- anneal
@@ -733,7 +808,10 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
         const int bond_u16 = (nbent + 7) & ~7;
         const bool lds_bonds = A.cm.bonds.ntype[s] <= kLdsBondTypes && nbent < 0xFFFF && bond_u16 <= sm.rest_cap;
         if (lds_bonds) {
-            for (int i = t; i < (int)A.cm.bonds.ntype[s]; i += NT) sm.btab[i] = bt[i];
+            for (int i = t; i < (int)A.cm.bonds.ntype[s]; i += NT) {
+                const float2 rk = bt[i];
+                sm.btab[i] = make_float4(rk.x * rk.x, 2.0f * rk.y * rk.x, -2.0f * rk.y, rk.y);
+            }
             for (int a = t; a < natom; a += NT) {
                 const uint32_t* g = adj + soff[a >> 6] + (a & 63);
                 uint16_t* o = sm.rest + sm.boff[a];
@@ -803,15 +881,13 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                 for (int b = 0; b < BPT; ++b) {
                     const int a = b * NT + t;
                     if (a < natom) {
-                        double ep = 0, eb = 0, ee[IGM_MAX_ENVELOPES] = {0, 0, 0, 0};
                         float fx, fy, fz;
                         const BondView B = lds_bonds ? BondView{nullptr, nullptr, sm.rest + sm.boff[a], sm.btab,
                                                                 (int)sm.boff[a + 1] - (int)sm.boff[a]}
                                                      : BondView{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
-                        atom_force<float, false, uint16_t, kLdsPairBatch>(s, a, sm.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], sm.pos, sm.L,
-                                                           pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
-                                                           pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz, ep,
-                                                           eb, ee);
+                        atom_force_md<kLdsPairBatch>(s, a, sm.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], sm.pos,
+                                                     sm.L, pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
+                                                     pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz);
 #pragma unroll
                         for (int i = 0; i < BPT; ++i)
                             if (b == i) {
