@@ -201,9 +201,10 @@ class Context(object):
 
     def mstep_profile(self):
         """cycle counters of the last anneal launch (IGM_PROF=1): dict of sums."""
-        out = (ctypes.c_ulonglong * 5)()
+        out = (ctypes.c_ulonglong * 6)()
         self.check(self.lib.igm_mstep_last_profile(self.h, out), 'igm_mstep_last_profile')
-        return dict(zip(('build_cycles', 'force_cycles', 'rest_cycles', 'evaluations', 'builds'), list(out)))
+        return dict(zip(('build_cycles', 'force_cycles', 'rest_cycles', 'evaluations', 'builds', 'walk_cycles'),
+                        list(out)))
 
     def close(self):
         if getattr(self, 'h', None):

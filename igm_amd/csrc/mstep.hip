@@ -323,9 +323,9 @@ __device__ __forceinline__ void walk27(int c, const OffT* cell, const uint16_t* 
 
 // Verlet list with skin from a cell grid.  Positions are read from `pos` (all
 // writers have passed a barrier).  The bead mask is pos.w >= 0.  Ends with a
-// barrier.
+// barrier.  Returns the clock cycles of the list-fill walk (profiling).
 template <typename T, int NT, typename OffT>
-__device__ __noinline__ void build_nlist(int natom, const vec4_t<T>* pos, NList<T, OffT> L, T cut_list, Red R) {
+__device__ __noinline__ unsigned long long build_nlist(int natom, const vec4_t<T>* pos, NList<T, OffT> L, T cut_list, Red R) {
     const int t = threadIdx.x;
     float mm[6];
 #pragma unroll
@@ -411,6 +411,7 @@ __device__ __noinline__ void build_nlist(int natom, const vec4_t<T>* pos, NList<
     }
     __syncthreads();
     const T cut2 = cut_list * cut_list;
+    const unsigned long long c_walk = clock64();
     // one pass: walk the 27 cells, write the list slots (the scratch above is dead)
     const int cap = L.kl + L.kg;
     for (int a = t; a < natom; a += NT) {
@@ -429,6 +430,226 @@ __device__ __noinline__ void build_nlist(int natom, const vec4_t<T>* pos, NList<
         L.nnb[a] = (uint16_t)(k <= cap ? k : kNnbWalk);
     }
     __syncthreads();
+    return clock64() - c_walk;
+}
+
+// LDS-path Verlet-list build of the anneal kernel: the algorithm and the list of
+// build_nlist (same grid, same cell order, ascending ids inside a cell, same slot
+// order -> bitwise the same list), written against address-space-qualified
+// pointers.  As a separate (non-inlined) function the generic pointers of NList
+// would compile to FLAT memory operations with full vmcnt+lgkmcnt waits and 64-bit
+// address arithmetic; here every scratch, grid and list access is a ds_* op and
+// the overflow slots are global stores.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define IGM_LDS __attribute__((address_space(3)))
+#define IGM_GLB __attribute__((address_space(1)))
+#else  // host pass: the kernels' bodies are not compiled for the host
+#define IGM_LDS
+#define IGM_GLB
+#endif
+typedef float igm_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 lds_f4(const IGM_LDS igm_f4v* p, int i) {
+    const igm_f4v v = p[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+template <int NT>
+__device__ __noinline__ unsigned long long build_nlist_lds(int natom, const float4* pos_g, NList<float, uint16_t> Lg,
+                                                           float cut_list, Red R) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    constexpr int NW = NT / 64;
+    const IGM_LDS igm_f4v* pos = (const IGM_LDS igm_f4v*)pos_g;
+    IGM_LDS uint16_t* cell = (IGM_LDS uint16_t*)Lg.cell;
+    IGM_LDS uint16_t* sorted = (IGM_LDS uint16_t*)Lg.sorted;
+    IGM_LDS uint16_t* nnb = (IGM_LDS uint16_t*)Lg.nnb;
+    IGM_LDS uint16_t* lell = (IGM_LDS uint16_t*)Lg.lell;
+    IGM_GLB uint16_t* gell = (IGM_GLB uint16_t*)Lg.gell;
+    IGM_LDS int* cnt = (IGM_LDS int*)Lg.scratch;
+    IGM_LDS float* redf = (IGM_LDS float*)R.redb;  // NW * 6 floats
+    IGM_LDS int* wsum = (IGM_LDS int*)R.wsum;
+    IGM_LDS float* gp = (IGM_LDS float*)Lg.gp;
+    IGM_LDS int* gn = (IGM_LDS int*)Lg.gn;
+    const int lstride = Lg.lstride, kl = Lg.kl, kg = Lg.kg, cap = kl + kg;
+    // bounding box of the beads (max of -x and x: exact in f32)
+    float mm[6];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) mm[d] = -3.0e38f;
+    for (int a = t; a < natom; a += NT) {
+        const float4 p = lds_f4(pos, a);
+        if (!(p.w >= 0.0f)) continue;
+        mm[0] = fmaxf(mm[0], -p.x);
+        mm[1] = fmaxf(mm[1], -p.y);
+        mm[2] = fmaxf(mm[2], -p.z);
+        mm[3] = fmaxf(mm[3], p.x);
+        mm[4] = fmaxf(mm[4], p.y);
+        mm[5] = fmaxf(mm[5], p.z);
+    }
+#pragma unroll
+    for (int d = 0; d < 6; ++d)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mm[d] = fmaxf(mm[d], __shfl_xor(mm[d], off));
+    if (lane == 0)
+#pragma unroll
+        for (int d = 0; d < 6; ++d) redf[w * 6 + d] = mm[d];
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        float v = redf[d];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) v = fmaxf(v, redf[i * 6 + d]);
+        mm[d] = v;
+    }
+    // grid (identical in every thread and to build_nlist): cells of side >= cut_list
+    float lo[3], inv[3];
+    int nb[3];
+    {
+        float ext[3], vol = 1.0f;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            ext[d] = mm[3 + d] + mm[d];
+            if (!(ext[d] >= 0.0f)) ext[d] = 0.0f;
+            vol *= fmaxf(ext[d], cut_list);
+        }
+        float cs = cut_list;
+        if (vol / (cs * cs * cs) > (float)Lg.cellcap) cs = cbrtf(vol / (float)Lg.cellcap) * 1.0001f;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = -mm[d];
+            nb[d] = (int)floorf(ext[d] / cs);
+            if (nb[d] < 1) nb[d] = 1;
+            inv[d] = ext[d] > 0.0f ? (float)nb[d] / ext[d] : 0.0f;
+        }
+    }
+    const int ncell = nb[0] * nb[1] * nb[2];
+    if (t == 0) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            gp[d] = lo[d];
+            gp[3 + d] = inv[d];
+            gn[d] = nb[d];
+        }
+    }
+    auto cell_of = [&](const float4& p) {
+        int ci[3];
+        const float pp[3] = {p.x, p.y, p.z};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int v = (int)((pp[d] - lo[d]) * inv[d]);
+            ci[d] = v < 0 ? 0 : (v >= nb[d] ? nb[d] - 1 : v);
+        }
+        return (ci[2] * nb[1] + ci[1]) * nb[0] + ci[0];
+    };
+    IGM_LDS int* slot = cnt + ncell + 1;
+    for (int c = t; c <= ncell; c += NT) cnt[c] = 0;
+    __syncthreads();
+    for (int a = t; a < natom; a += NT) {
+        const float4 p = lds_f4(pos, a);
+        if (!(p.w >= 0.0f)) continue;
+        slot[a] = __hip_atomic_fetch_add(&cnt[cell_of(p)], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    {  // exclusive scan of the counts: cell[c] = sum_{c' < c} cnt[c'], cell[ncell] = total
+        const int cpt = (ncell + NT - 1) / NT, beg = t * cpt;
+        int s = 0;
+        for (int i = 0; i < cpt; ++i)
+            if (beg + i < ncell) s += cnt[beg + i];
+        int incl = s;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        int woff = 0, total = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const int v = wsum[i];
+            woff += i < w ? v : 0;
+            total += v;
+        }
+        int run = woff + incl - s;
+        for (int i = 0; i < cpt; ++i) {
+            const int idx = beg + i;
+            if (idx < ncell) {
+                const int v = cnt[idx];
+                cnt[idx] = run;
+                cell[idx] = (uint16_t)run;
+                run += v;
+            }
+        }
+        if (t == 0) {
+            cnt[ncell] = total;
+            cell[ncell] = (uint16_t)total;
+        }
+        __syncthreads();
+    }
+    for (int a = t; a < natom; a += NT) {
+        const float4 p = lds_f4(pos, a);
+        if (!(p.w >= 0.0f)) continue;
+        sorted[cnt[cell_of(p)] + slot[a]] = (uint16_t)a;
+    }
+    __syncthreads();
+    for (int c = t; c < ncell; c += NT) {  // deterministic order inside each cell
+        const int beg = (int)cell[c], end = (int)cell[c + 1];
+        for (int i = beg + 1; i < end; ++i) {
+            const uint16_t v = sorted[i];
+            int k = i - 1;
+            while (k >= beg && sorted[k] > v) {
+                sorted[k + 1] = sorted[k];
+                --k;
+            }
+            sorted[k + 1] = v;
+        }
+    }
+    __syncthreads();
+    const float cut2 = cut_list * cut_list;
+    const unsigned long long c_walk = clock64();
+    // one pass: walk the 27 cells (9 x-runs of consecutive sorted slots), write the
+    // list slots (the count scratch above is dead)
+    const int nx = nb[0], ny = nb[1], nz = nb[2];
+    for (int a = t; a < natom; a += NT) {
+        const float4 p0 = lds_f4(pos, a);
+        int k = 0;
+        if (p0.w >= 0.0f) {
+            const int c = cell_of(p0);
+            const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+            const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
+            for (int dz = -1; dz <= 1; ++dz) {
+                const int z0 = cz + dz;
+                if (z0 < 0 || z0 >= nz) continue;
+                for (int dy = -1; dy <= 1; ++dy) {
+                    const int y0 = cy + dy;
+                    if (y0 < 0 || y0 >= ny) continue;
+                    const int row = (z0 * ny + y0) * nx;
+                    const int beg = (int)cell[row + xlo], end = (int)cell[row + xhi + 1];
+                    for (int q = beg; q < end; q += IGM_WALK_BATCH) {
+                        int jj[IGM_WALK_BATCH];
+#pragma unroll
+                        for (int u = 0; u < IGM_WALK_BATCH; ++u) jj[u] = (int)sorted[q + u < end ? q + u : beg];
+                        float4 pj[IGM_WALK_BATCH];
+#pragma unroll
+                        for (int u = 0; u < IGM_WALK_BATCH; ++u) pj[u] = lds_f4(pos, jj[u]);
+#pragma unroll
+                        for (int u = 0; u < IGM_WALK_BATCH; ++u) {
+                            const float ddx = p0.x - pj[u].x, ddy = p0.y - pj[u].y, ddz = p0.z - pj[u].z;
+                            const bool in = q + u < end && jj[u] != a && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
+                            if (in) {
+                                if (k < kl)
+                                    lell[k * lstride + a] = (uint16_t)jj[u];
+                                else if (k < cap)
+                                    gell[((a >> 6) * kg + (k - kl)) * 64 + (a & 63)] = (uint16_t)jj[u];
+                            }
+                            k += in ? 1 : 0;
+                        }
+                    }
+                }
+            }
+        }
+        nnb[a] = (uint16_t)(k <= cap ? k : kNnbWalk);
+    }
+    __syncthreads();
+    return clock64() - c_walk;
 }
 
 // ------------------------------------------------------------- forces
@@ -772,6 +993,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
         if (s >= A.cm.nstruct) break;
         const float* xs = A.xyz + (size_t)s * natom * 3;
         uint32_t mobile = 0u;  // bit b: atom b*NT+t is integrated
+        uint32_t flk = 0u;     // 5 bits per atom b: FIXED, ENV0..ENV3 (the flags the force reads)
         int nmob = 0;
 #pragma unroll
         for (int b = 0; b < BPT; ++b) {
@@ -779,6 +1001,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
             const bool in = a < natom;
             const uint32_t fl = in ? A.cm.aflags[(size_t)s * A.cm.afs + a] : 0u;
             const bool bead = in && (fl & IGM_ATOM_BEAD);
+            flk |= (((fl & IGM_ATOM_FIXED) ? 1u : 0u) | (((fl >> 4) & 0xfu) << 1)) << (5 * b);
             if (in && !(fl & IGM_ATOM_FIXED)) {
                 mobile |= 1u << b;
                 ++nmob;
@@ -824,7 +1047,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
         }
         __syncthreads();
         int nbuild = 0;
-        unsigned long long c_build = 0, c_force = 0, c_all = 0, nstep_total = 0;
+        unsigned long long c_build = 0, c_force = 0, c_all = 0, nstep_total = 0, c_walk = 0;
         const unsigned long long c_begin = A.prof ? clock64() : 0;
         for (int seg = 0; seg < A.nseg; ++seg) {
             const float* vsrc = A.mode == 1 ? A.vel + (size_t)s * natom * 3
@@ -863,8 +1086,11 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                 }
                 if (__syncthreads_or(moved)) {  // neigh_modify every 1 check yes
                     const unsigned long long c0 = A.prof ? clock64() : 0;
-                    build_nlist<float, NT, uint16_t>(natom, sm.pos, sm.L, A.P.cut_list, sm.r);
-                    if (A.prof) c_build += clock64() - c0;
+                    const unsigned long long cw = build_nlist_lds<NT>(natom, sm.pos, sm.L, A.P.cut_list, sm.r);
+                    if (A.prof) {
+                        c_build += clock64() - c0;
+                        c_walk += cw;
+                    }
                     ++nbuild;
 #pragma unroll
                     for (int b = 0; b < BPT; ++b) {
@@ -885,7 +1111,9 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                         const BondView B = lds_bonds ? BondView{nullptr, nullptr, sm.rest + sm.boff[a], sm.btab,
                                                                 (int)sm.boff[a + 1] - (int)sm.boff[a]}
                                                      : BondView{adj + soff[a >> 6] + lane, bt, nullptr, nullptr, deg[a]};
-                        atom_force_md<kLdsPairBatch>(s, a, sm.pos[a], A.cm.aflags[(size_t)s * A.cm.afs + a], sm.pos,
+                        const uint32_t f5 = (flk >> (5 * b)) & 31u;
+                        const uint32_t fla = ((f5 & 1u) ? IGM_ATOM_FIXED : 0u) | ((f5 >> 1) << 4);
+                        atom_force_md<kLdsPairBatch>(s, a, sm.pos[a], fla, sm.pos,
                                                      sm.L, pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
                                                      pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz);
 #pragma unroll
@@ -950,6 +1178,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
             atomicAdd(&A.prof[2], c_all - c_build - c_force);
             atomicAdd(&A.prof[3], nstep_total);
             atomicAdd(&A.prof[4], (unsigned long long)nbuild);
+            atomicAdd(&A.prof[5], c_walk);
         }
         __syncthreads();
     }
@@ -3245,15 +3474,15 @@ extern "C" int igm_mstep_set_volumes(igm_ctx* c, int32_t nmap, const igm_volume_
 }
 
 /* Profiling aid (IGM_PROF=1 in the environment): cycle counters of the last LDS-path
- * anneal launch summed over structures: {build, force, rest, steps, builds}. */
+ * anneal launch summed over structures: {build, force, rest, steps, builds, list-fill walk}. */
 extern "C" int igm_mstep_last_profile(igm_ctx* c, unsigned long long* out) {
     if (!c || !out) return IGM_E_INVALID;
     auto it = c->ws.find("ms_prof");
     if (it == c->ws.end() || !it->second.first) {
-        memset(out, 0, sizeof(unsigned long long) * 5);
+        memset(out, 0, sizeof(unsigned long long) * 6);
         return IGM_OK;
     }
-    IGM_HIP_CHECK(c, hipMemcpyAsync(out, it->second.first, sizeof(unsigned long long) * 5, hipMemcpyDeviceToHost,
+    IGM_HIP_CHECK(c, hipMemcpyAsync(out, it->second.first, sizeof(unsigned long long) * 6, hipMemcpyDeviceToHost,
                                     c->stream));
     IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
     return IGM_OK;

@@ -363,8 +363,9 @@ int igm_velocity_create(igm_ctx* ctx, uint32_t flags, int32_t nseed, int32_t nat
                         float* v);
 
 /* Profiling aid: with IGM_PROF set in the environment, the LDS-path anneal kernel
- * accumulates shader-clock cycles; out[5] = {neighbour builds, force phases, rest,
- * force evaluations, builds} summed over the structures of the last launch. */
+ * accumulates shader-clock cycles; out[6] = {neighbour builds, force phases, rest,
+ * force evaluations, builds, list-fill walks (part of the builds)} summed over the
+ * structures of the last launch. */
 int igm_mstep_last_profile(igm_ctx* ctx, unsigned long long* out);
 
 /* ---- M-step restraint assembly: Hi-C contact selection ---------------------

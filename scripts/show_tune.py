@@ -9,4 +9,6 @@ for f in sorted(glob.glob('gpurun_out/tune_*.log')):
                 tot = p['build_cycles'] + p['force_cycles'] + p['rest_cycles']
                 s += ' | cyc/eval %.0f build %.2f force %.2f rest %.2f' % (tot / p['evaluations'], p['build_cycles'] / tot,
                                                                        p['force_cycles'] / tot, p['rest_cycles'] / tot)
+                if p.get('walk_cycles'):
+                    s += ' walk %.2f cyc/build %.0f' % (p['walk_cycles'] / tot, p['build_cycles'] / max(p['builds'], 1))
             print(s)
