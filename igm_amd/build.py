@@ -32,6 +32,9 @@ SOURCES = {
     'asteps.hip': ['-ffp-contract=off'],
     'restraints.hip': ['-ffp-contract=off'],
 }
+# host-only C++ (no device code): the .hss / actdist.hdf5 reader and writer
+HOST_SOURCES = {'h5io.cpp': []}
+LIBS = ['-lz']
 COMMON = ['-O3', '-fPIC', '-std=c++17', '--offload-arch=%s' % ARCH, '-Wall', '-Wno-unused-function',
           '-munsafe-fp-atomics', '-I%s' % os.path.join(ROOT, 'include')]
 
@@ -47,7 +50,7 @@ def build_lib(verbose=False):
     os.makedirs(OBJDIR, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
-    headers.append(os.path.join(ROOT, 'include', 'igm_hip.h'))
+    headers += [os.path.join(ROOT, 'include', h) for h in ('igm_hip.h', 'igm_io.h')]
     jobs = []
     objs = []
     for src, extra in SOURCES.items():
@@ -58,6 +61,13 @@ def build_lib(verbose=False):
         objs.append(op)
         if _newer(op, [sp] + headers):
             jobs.append([HIPCC] + COMMON + extra + ['-c', sp, '-o', op])
+    for src, extra in HOST_SOURCES.items():
+        sp = os.path.join(CSRC, src)
+        op = os.path.join(OBJDIR, src.replace('.cpp', '.o'))
+        objs.append(op)
+        if _newer(op, [sp] + headers):
+            jobs.append(['g++', '-O2', '-fPIC', '-std=c++17', '-Wall', '-Wextra', '-Wno-unused-parameter',
+                         '-I%s' % os.path.join(ROOT, 'include')] + extra + ['-c', sp, '-o', op])
 
     def run(cmd):
         if verbose:
@@ -72,7 +82,7 @@ def build_lib(verbose=False):
             if verbose and out.strip():
                 print(out)
     if jobs or not os.path.exists(LIB):
-        run([HIPCC, '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', LIB] + objs)
+        run([HIPCC, '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', LIB] + objs + LIBS)
     return LIB
 
 

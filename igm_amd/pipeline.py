@@ -244,6 +244,72 @@ class AMIteration(object):
         self.times = {'astep_s': t1 - t0, 'mstep_s': t2 - t1}
         return self.times
 
+    # ------------------------------------------------------------------ checkpoint
+    def checkpoint(self, path):
+        """Write the loop state to a .hss (igm_amd.hss layout; collective when world > 1,
+        rank 0 writes): the population bead-major like the reference's .hss after a
+        ModelingStep (ModelingStep.py:578-610), and under 'igm_amd/' what the next
+        iteration needs -- step_no (the LAMMPS seeds), every pair with its plast (the
+        it_corr state of ActivationDistanceStep), the non-bead atoms' coordinates."""
+        from . import hss
+        P = _lib.ptr
+        src = gather_population(self.xyz, self.group) if self.world > 1 else self.xyz
+        self._call('igm_population_transpose', IGM_DEVICE_PTRS, self.nbead, self.S_total, self.natom, P(src),
+                   P(self.pop_bm), 1)
+        pairs_u8 = self.pairs[:self.npairs * pair_dtype.itemsize]
+        if self.world > 1:
+            pairs_u8, np_tot = gather_rows(pairs_u8, self.npairs, pair_dtype.itemsize, self.group)
+            pairs_u8 = pairs_u8[:np_tot * pair_dtype.itemsize]
+        self._sync()
+        if self.rank != 0:
+            return
+        crd = self.pop_bm.cpu().numpy()
+        extra = src[:, self.nbead:, :].cpu().numpy()
+        pairs = pairs_u8.cpu().numpy().view(pair_dtype)
+        cp, ci = self.copy_ptr.cpu().numpy(), self.copy_idx.cpu().numpy()
+        chrom = self.chrom.cpu().numpy()[:self.nbead]
+        copy = np.zeros(self.nbead, np.int32)
+        for h in range(len(cp) - 1):
+            copy[ci[cp[h]:cp[h + 1]]] = np.arange(cp[h + 1] - cp[h], dtype=np.int32)
+        from . import h5
+        tree = {'@version': np.int32(2), '@violation': np.float64(self.violation_score() if hasattr(self, 'stats')
+                                                                   else np.nan),
+                '@nstruct': np.int64(self.S_total), '@nbead': np.int64(self.nbead),
+                'coordinates': crd, 'radii': self.bead_radii.cpu().numpy(),
+                'index': hss.index_tree(chrom, copy, cp, ci),
+                'igm_amd': {'@step_no': np.int64(self.step_no), 'extra_atoms': extra,
+                            'pair_i': pairs['i'], 'pair_j': pairs['j'], 'pwish': pairs['pwish'],
+                            'plast': pairs['plast']}}
+        h5.write(path, tree)
+
+    def restore(self, path):
+        """Load a checkpoint() of the same population and pair list (this rank's
+        structures and pair shard): the next step() continues the interrupted run."""
+        from . import h5
+        torch = self.torch
+        with h5.File(path) as f:
+            if int(f.attrs('/')['nstruct']) != self.S_total or int(f.attrs('/')['nbead']) != self.nbead:
+                raise ValueError('checkpoint %s holds a different population' % path)
+            crd = f.read('coordinates')
+            extra = f.read('igm_amd/extra_atoms')
+            step_no = int(f.attrs('igm_amd')['step_no'])
+            pi, pj, plast = f.read('igm_amd/pair_i'), f.read('igm_amd/pair_j'), f.read('igm_amd/plast')
+        if len(pi) != self.npairs_total:
+            raise ValueError('checkpoint %s holds a different pair list' % path)
+        s0 = int(self.sids[0])
+        x = np.zeros((self.S_local, self.natom, 3), np.float32)
+        x[:, :self.nbead] = crd[:, s0:s0 + self.S_local].transpose(1, 0, 2)
+        x[:, self.nbead:] = extra[s0:s0 + self.S_local]
+        self.xyz.copy_(torch.from_numpy(x))
+        pairs = self.pairs[:self.npairs * pair_dtype.itemsize].cpu().numpy().view(pair_dtype).copy()
+        lo, hi = self.pair_lo, self.pair_hi
+        if not (np.array_equal(pairs['i'], pi[lo:hi]) and np.array_equal(pairs['j'], pj[lo:hi])):
+            raise ValueError('checkpoint %s holds a different pair list' % path)
+        pairs['plast'] = plast[lo:hi]
+        if self.npairs:
+            self.pairs[:self.npairs * pair_dtype.itemsize].copy_(torch.from_numpy(pairs.view(np.uint8)))
+        self.step_no = step_no
+
     def info_host(self):
         return self.info.cpu().numpy().view(optinfo_dtype)
 

@@ -21,14 +21,16 @@ scheduler instead of ipyparallel, restartable at batch granularity.
                   the A-step (ActivationDistanceStep.py:42-298) and M-step
                   (ModelingStep.py:105-783) on the GPU kernels of this package.
 
-Storage.  The reference keeps the population in alabtools' .hss (HDF5) and the
-rows in actdist.hdf5; h5py is not importable by this package's Python, so the same
-arrays live in numpy files with the reference's layouts: `<structure_output>.npy`
-= the .hss 'coordinates' dataset (nbead, nstruct, 3) float32 (bead-major), with the
-index / radii in `<structure_output>.index.npz`; `actdist.npz` = {row, col, dist,
-prob} of actdist.hdf5.  The kernels behind the steps are looked up by name in
-KERNELS (cfg optimization/kernel, default 'hip'); the product registers only the
-GPU kernels.
+Storage.  The population, the Hi-C input and the A-step rows are the reference's own
+HDF5 files, read and written by the native reader/writer of this package (igm_amd.h5
+over csrc/h5io.cpp; h5py is not importable here): `<structure_output>` ending in
+.hss is an alabtools HssFile (coordinates (nbead, nstruct, 3) float32 bead-major,
+index, radii, summary), `input_matrix` a .hcs Contactmatrix, `actdist_file` an
+actdist.hdf5 {row, col, dist, prob}.  Files this package writes are contiguous, so
+the coordinates are memory-mapped and the M-step's reduce updates them in place.
+Other extensions keep the same arrays in numpy files (`<out>.npy` + `<out>.index.npz`,
+`.npz` rows / CSR).  The kernels behind the steps are looked up by name in KERNELS
+(cfg optimization/kernel, default 'hip'); the product registers only the GPU kernels.
 """
 import hashlib
 import json
@@ -288,33 +290,85 @@ class Step(object):
 # ------------------------------------------------------------------ population store
 class PopulationStore(object):
     """The .hss arrays the steps read and write: coordinates (nbead, nstruct, 3) float32
-    bead-major (core/step.py:373, _preprocess.py:103-105) as a memory-mapped .npy, and
-    the index (radii, chrom, copy, copy_ptr/copy_idx of index.copy_index, chrom_sizes)."""
+    bead-major (core/step.py:373, _preprocess.py:103-105) and the index (radii, chrom,
+    copy, copy_ptr/copy_idx of index.copy_index, the haploid chrom).  A path ending in
+    .hss is the HDF5 HssFile itself (igm_amd.hss); otherwise numpy files."""
 
     def __init__(self, path):
         self.path = path
-        meta = np.load(path + '.index.npz')
-        self.radii = meta['radii'].astype(np.float32)
-        self.chrom = meta['chrom'].astype(np.int32)
-        self.copy = meta['copy'].astype(np.int32)
-        self.copy_ptr = meta['copy_ptr'].astype(np.int32)
-        self.copy_idx = meta['copy_idx'].astype(np.int32)
-        self.hap_chrom = meta['hap_chrom'].astype(np.int32) if 'hap_chrom' in meta else self.chrom
+        self.is_hss = path.endswith('.hss')
+        if self.is_hss:
+            from . import hss
+            h = hss.Hss(path)
+            self.radii, self.chrom, self.copy = h.radii, h.chrom, h.copy
+            self.copy_ptr, self.copy_idx = h.copy_ptr, h.copy_idx
+            self.hap_chrom = self.chrom[self.copy_idx[self.copy_ptr[:-1]]]
+        else:
+            meta = np.load(path + '.index.npz')
+            self.radii = meta['radii'].astype(np.float32)
+            self.chrom = meta['chrom'].astype(np.int32)
+            self.copy = meta['copy'].astype(np.int32)
+            self.copy_ptr = meta['copy_ptr'].astype(np.int32)
+            self.copy_idx = meta['copy_idx'].astype(np.int32)
+            self.hap_chrom = meta['hap_chrom'].astype(np.int32) if 'hap_chrom' in meta else self.chrom
         self.nbead = len(self.radii)
 
     @staticmethod
     def create(path, coordinates, radii, chrom, copy, copy_ptr, copy_idx, hap_chrom=None):
+        if path.endswith('.hss'):
+            from . import hss
+            hss.write_hss(path, coordinates, radii, hss.index_tree(chrom, copy, copy_ptr, copy_idx))
+            return PopulationStore(path)
         np.savez(path + '.index.npz', radii=radii, chrom=chrom, copy=copy, copy_ptr=copy_ptr, copy_idx=copy_idx,
                  hap_chrom=chrom if hap_chrom is None else hap_chrom)
         np.save(path + '.npy', np.ascontiguousarray(coordinates, np.float32))
         return PopulationStore(path)
 
     def coordinates(self, mode='r'):
+        if self.is_hss:
+            from . import hss
+            return hss.coordinates_memmap(self.path, mode)
         return np.load(self.path + '.npy', mmap_mode=mode)
 
     @property
     def nstruct(self):
         return self.coordinates().shape[1]
+
+    def write_summary(self, text, violation):
+        """the population summary (ModelingStep.py:700-726: hss 'summary' + 'violation')"""
+        if self.is_hss:
+            from . import hss
+            hss.update_hss(self.path, summary=text, violation=violation)
+        else:
+            with open(self.path + '.summary.json', 'w') as f:
+                f.write(text)
+
+    def read_summary(self):
+        if self.is_hss:
+            from . import hss
+            return hss.Hss(self.path).summary
+        with open(self.path + '.summary.json') as f:
+            return f.read()
+
+
+def read_rows(path):
+    """the A-step rows of an actdist file (actdist.hdf5, or the .npz form)"""
+    if path.endswith('.npz'):
+        d = np.load(path)
+        rows = np.zeros(len(d['row']), row_dtype)
+        for k in ('row', 'col', 'dist', 'prob'):
+            rows[k] = d[k]
+        return rows
+    from . import hss
+    return hss.read_actdist(path)
+
+
+def read_input_matrix(path):
+    """the .hcs CSR arrays (indptr, indices, data, chrom) of restraints/Hi-C/input_matrix"""
+    if path.endswith('.npz'):
+        return dict(np.load(path))
+    from . import hss
+    return hss.read_hcs(path)
 
 
 # ------------------------------------------------------------------ kernels
@@ -402,14 +456,9 @@ class ActivationDistanceStep(Step):
 
     def setup(self):
         from . import astep
-        hic = np.load(self.cfg['restraints']['Hi-C']['input_matrix'])  # .hcs arrays: indptr, indices, data, chrom
+        hic = read_input_matrix(self.cfg['restraints']['Hi-C']['input_matrix'])  # indptr, indices, data, chrom
         last = cget(self.cfg, 'runtime/Hi-C/actdist_file', None)
-        last_rows = None
-        if last is not None and os.path.isfile(last):
-            d = np.load(last)
-            last_rows = np.zeros(len(d['row']), row_dtype)
-            for k in ('row', 'col', 'dist', 'prob'):
-                last_rows[k] = d[k]
+        last_rows = read_rows(last) if last is not None and os.path.isfile(last) else None
         pairs = astep.select_pairs(hic['indptr'], hic['indices'], hic['data'], hic['chrom'],
                                    cget(self.cfg, 'runtime/Hi-C/intra_sigma', False),
                                    cget(self.cfg, 'runtime/Hi-C/inter_sigma', False), last_rows=last_rows)
@@ -431,20 +480,24 @@ class ActivationDistanceStep(Step):
         os.replace(tmp, batch['out'])
 
     def reduce(self):
-        """concatenate in batch order (= CSR pair order) -> actdist.npz; the previous
-        file is rotated like ActivationDistanceStep.py:292-295."""
+        """concatenate in batch order (= CSR pair order) -> actdist.hdf5 (:285-289); the
+        previous file is rotated like ActivationDistanceStep.py:292-295."""
         rows = np.concatenate([np.load(b['out']) for b in self.argument_list]) if self.argument_list else \
             np.zeros(0, row_dtype)
         out = os.path.join(cget(self.cfg, 'parameters/workdir', '.'),
-                           cget(self.cfg, 'restraints/Hi-C/actdist_file', 'actdist.npz'))
+                           cget(self.cfg, 'restraints/Hi-C/actdist_file', 'actdist.hdf5'))
         last = cget(self.cfg, 'runtime/Hi-C/actdist_file', None)
         if last is not None and os.path.isfile(last) and os.path.abspath(last) == os.path.abspath(out):
             os.replace(last, '%s.INTERsigma_%.4f_INTRAsigma_%.4f_iter_%s' % (
                 out, cget(self.cfg, 'runtime/Hi-C/inter_sigma'), cget(self.cfg, 'runtime/Hi-C/intra_sigma'),
                 str(cget(self.cfg, 'runtime/opt_iter', 0))))
-        tmp = out + '.part.npz'
-        np.savez(tmp, row=rows['row'], col=rows['col'], dist=rows['dist'], prob=rows['prob'])
-        os.replace(tmp, out)
+        if out.endswith('.npz'):
+            tmp = out + '.part.npz'
+            np.savez(tmp, row=rows['row'], col=rows['col'], dist=rows['dist'], prob=rows['prob'])
+            os.replace(tmp, out)
+        else:
+            from . import hss
+            hss.write_actdist(out, rows)
         cset(self.cfg, 'runtime/Hi-C/actdist_file', out)
 
 
@@ -463,11 +516,7 @@ class ModelingStep(Step):
     def task(self, batch, device):
         store = PopulationStore(self.cfg['optimization']['structure_output'])
         act = cget(self.cfg, 'runtime/Hi-C/actdist_file', None)
-        d = np.load(act) if act else None
-        rows = np.zeros(0 if d is None else len(d['row']), row_dtype)
-        if d is not None:
-            for k in ('row', 'col', 'dist', 'prob'):
-                rows[k] = d[k]
+        rows = read_rows(act) if act else np.zeros(0, row_dtype)
         res = _kernel(self.cfg, 'mstep')(store, np.asarray(batch['sids']), rows, self.cfg, device)
         tmp = batch['out'] + '.part.npz'
         np.savez(tmp, xyz=res['xyz'], info=res['info'].view(np.uint8), stats=res['stats'])
@@ -500,6 +549,6 @@ class ModelingStep(Step):
                 summ.set_structure(sid, vstat_from_record(res['stats'][q], names), opt)
         crd.flush()
         del crd
-        with open(self.cfg['optimization']['structure_output'] + '.summary.json', 'w') as f:
-            f.write(summ.to_json())
-        cset(self.cfg, 'runtime/violation_score', float(summ.violation_score()))
+        score = float(summ.violation_score())
+        store.write_summary(summ.to_json(), score)
+        cset(self.cfg, 'runtime/violation_score', score)

@@ -7,8 +7,8 @@ import re
 from conftest import ROOT
 
 
-def declared_functions():
-    src = open(os.path.join(ROOT, 'include', 'igm_hip.h')).read()
+def declared_functions(header='igm_hip.h'):
+    src = open(os.path.join(ROOT, 'include', header)).read()
     src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
     names = re.findall(r'^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_ ]*[\s\*]+(igm_[a-z0-9_]+)\s*\(', src, flags=re.M)
     return sorted(set(names))
@@ -49,3 +49,16 @@ def test_no_gpu_means_loud_failure():
         pytest.skip('GPU present')
     with pytest.raises(RuntimeError):
         _lib.Context(0)
+
+
+def test_io_library_exports_all_declared_symbols():
+    """include/igm_io.h (the native .hss / actdist.hdf5 I/O) is exported by the same
+    library and bound symbol for symbol in igm_amd.h5"""
+    from igm_amd import _lib, h5
+    lib = _lib.load()
+    names = declared_functions('igm_io.h')
+    assert 'igm_h5_open' in names and 'igm_h5w_close' in names
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, 'libigmhip.so is missing %s' % missing
+    assert set(names) == set(h5.SIGNATURES)
+    h5.lib()

@@ -60,14 +60,25 @@ def _oracle_mstep(store, sids, rows, cfg, device):
 ST.KERNELS['cpu_oracle_test'] = {'actdist': _oracle_actdist, 'mstep': _oracle_mstep}
 
 
-def _setup(tmp, S=9):
+def _setup(tmp, S=9, fmt='hdf5'):
+    """fmt 'hdf5': the reference's own files (.hcs input, .hss population, actdist.hdf5)
+    through the native HDF5 reader/writer; 'npy': the numpy-file form"""
     pop = np.load(os.path.join(GOLDEN, 'demo_population.npz'))
     hic = np.load(os.path.join(GOLDEN, 'demo_hic_pairs.npz'))
     nhap = int(hic['nhap'])
-    hcs = os.path.join(tmp, 'input.hcs.npz')
     indptr = np.concatenate([[0], np.cumsum(np.bincount(hic['i'], minlength=nhap))])
-    np.savez(hcs, indptr=indptr, indices=hic['j'], data=hic['p'], chrom=pop['hap_chrom'])
-    out = os.path.join(tmp, 'igm-model')
+    if fmt == 'hdf5':
+        from igm_amd import h5
+        hcs = os.path.join(tmp, 'input.hcs')
+        h5.write(hcs, {'@nbin': np.int64(nhap), '@version': '0.0.4',
+                       'matrix': {'indptr': indptr.astype(np.int32), 'indices': hic['j'].astype(np.int32),
+                                  'data': hic['p'].astype(np.float32)},
+                       'index': {'chrom': pop['hap_chrom'].astype(np.int32)}})
+        out, act = os.path.join(tmp, 'igm-model.hss'), 'actdist.hdf5'
+    else:
+        hcs = os.path.join(tmp, 'input.hcs.npz')
+        np.savez(hcs, indptr=indptr, indices=hic['j'], data=hic['p'], chrom=pop['hap_chrom'])
+        out, act = os.path.join(tmp, 'igm-model'), 'actdist.npz'
     ST.PopulationStore.create(out, pop['coordinates'][:, :S], pop['radii'], pop['chrom'], pop['copy'],
                               pop['copy_ptr'], pop['copy_idx'])
     cfg = {'parameters': {'workdir': tmp, 'tmp_dir': 'tmp', 'step_db': os.path.join(tmp, 'stepdb.sqlite')},
@@ -77,7 +88,7 @@ def _setup(tmp, S=9):
                                     'envelope': {'nucleus_shape': 'sphere', 'nucleus_radius': 5500,
                                                  'nucleus_kspring': 1.0}}},
            'restraints': {'Hi-C': {'input_matrix': hcs, 'intra_sigma_list': [1.0, 0.2], 'inter_sigma_list': [1.0, 0.2],
-                                   'contact_range': 2.0, 'contact_kspring': 1.0, 'actdist_file': 'actdist.npz'}},
+                                   'contact_range': 2.0, 'contact_kspring': 1.0, 'actdist_file': act}},
            'optimization': {'structure_output': out, 'kernel': 'cpu_oracle_test', 'iter_corr_knob': 1,
                             'kernel_opts': {'hip': {'batch_size': 3, 'pair_batch': 500, 'devices': [0]}},
                             'optimizer_options': MS.scaled_protocol(F.DEMO_PROTOCOL, 0.002)},
@@ -89,9 +100,10 @@ def _statuses(db, uid):
     return [x['status'] for x in ST.StepDB(db).get_history(uid)]
 
 
-def test_iteration_chain_and_stepdb(tmp_path):
+@pytest.mark.parametrize('fmt', ['hdf5', 'npy'])
+def test_iteration_chain_and_stepdb(tmp_path, fmt):
     tmp = str(tmp_path)
-    cfg = _setup(tmp)
+    cfg = _setup(tmp, fmt=fmt)
     del CALLS[:]
     a = ST.ActivationDistanceStep(cfg)
     a.run()
@@ -99,7 +111,7 @@ def test_iteration_chain_and_stepdb(tmp_path):
     assert _statuses(db, a.uid) == ['entry', 'setup', 'map', 'mapped', 'reduced', 'cleanup', 'completed']
     assert cfg['runtime']['Hi-C']['intra_sigma'] == 1.0 and cfg['runtime']['Hi-C']['intra_sigma_list'] == [0.2]
     # the rows: the pair batches in order == one oracle pass over every selected pair
-    act = np.load(cfg['runtime']['Hi-C']['actdist_file'])
+    act = ST.read_rows(cfg['runtime']['Hi-C']['actdist_file'])
     assert len(a.argument_list) > 1
     pairs = np.concatenate([np.load(b['pairs']) for b in a.argument_list])
     store = ST.PopulationStore(cfg['optimization']['structure_output'])
@@ -113,8 +125,12 @@ def test_iteration_chain_and_stepdb(tmp_path):
     x1 = np.array(store.coordinates())
     assert not np.array_equal(x0, x1) and np.all(np.isfinite(x1))
     assert 'violation_score' in cfg['runtime']
-    summ = json.load(open(cfg['optimization']['structure_output'] + '.summary.json'))
+    summ = json.loads(store.read_summary())
     assert len(summ['bystructure']['total_energies']) == 9
+    if fmt == 'hdf5':  # the population file carries the score like the reference's .hss
+        from igm_amd import hss
+        h = hss.Hss(cfg['optimization']['structure_output'])
+        assert h.violation == cfg['runtime']['violation_score'] and h.nstruct == 9
     # the StepDB file has the reference schema: igm-run's restart code reads it
     with sqlite3.connect(db) as conn:
         cols = [(r[1], r[2]) for r in conn.execute('PRAGMA table_info(steps)')]
@@ -127,18 +143,19 @@ def test_iteration_chain_and_stepdb(tmp_path):
     assert CALLS == []
 
 
-def test_killed_mstep_resumes_without_redoing_batches(tmp_path):
+@pytest.mark.parametrize('fmt', ['hdf5', 'npy'])
+def test_killed_mstep_resumes_without_redoing_batches(tmp_path, fmt):
     # reference result: an uninterrupted A-step + M-step in its own directory
     ref_dir = tmp_path / 'ref'
     ref_dir.mkdir()
-    cfg_r = _setup(str(ref_dir))
+    cfg_r = _setup(str(ref_dir), fmt=fmt)
     ST.ActivationDistanceStep(cfg_r).run()
     ST.ModelingStep(cfg_r).run()
     x_ref = np.array(ST.PopulationStore(cfg_r['optimization']['structure_output']).coordinates())
 
     run_dir = tmp_path / 'run'
     run_dir.mkdir()
-    cfg = _setup(str(run_dir))
+    cfg = _setup(str(run_dir), fmt=fmt)
     ST.ActivationDistanceStep(cfg).run()
     before = copy.deepcopy(cfg)  # igm-run restores this runtime section from the StepDB on restart
     del CALLS[:]
@@ -187,7 +204,7 @@ def test_gpu_iteration_chain_with_hip_kernels(tmp_path):
     cfg = _setup(tmp)
     cfg['optimization']['kernel'] = 'hip'
     ST.ActivationDistanceStep(cfg).run()
-    act = np.load(cfg['runtime']['Hi-C']['actdist_file'])
+    act = ST.read_rows(cfg['runtime']['Hi-C']['actdist_file'])
     store = ST.PopulationStore(cfg['optimization']['structure_output'])
     a_pairs = [f for f in os.listdir(os.path.join(tmp, 'tmp')) if f.endswith('.in.npy')]
     assert a_pairs
@@ -197,6 +214,6 @@ def test_gpu_iteration_chain_with_hip_kernels(tmp_path):
     x1 = np.array(store.coordinates())
     assert np.all(np.isfinite(x1)) and not np.array_equal(x0, x1)
     assert 0.0 <= cfg['runtime']['violation_score'] < 0.5
-    summ = json.load(open(cfg['optimization']['structure_output'] + '.summary.json'))
+    summ = json.loads(store.read_summary())
     assert 'Envelope[shape=sphere,k=1.0,a=5500,b=5500,c=5500]' in summ['byrestraint']
     assert len(act['row']) > 100
