@@ -1214,6 +1214,17 @@ constexpr int kFillW = IGM_POP_FILL_W;  // list build: slots per x-run loaded in
 #define IGM_POP_LIST_CAP 48  // measured on config C: 48 beats 64 (fill occupancy) and 40 (more cell walks)
 #endif
 constexpr int kPopListCap = IGM_POP_LIST_CAP;  // Verlet-list entries per slot (more: the cell walk)
+#ifndef IGM_POP_PREFETCH
+#define IGM_POP_PREFETCH 1  // force kernel: software-pipelined list quads, bond entries with the slot's loads
+#endif
+#ifndef IGM_POP_FUSED
+// 1: list build + bond re-index inside the force kernel of a rebuild step.  Measured
+// on config C (protocol x0.1, same box): fused -1.8 % anneal alone, but with the
+// prefetching force kernel its 80 VGPRs spill and the pair is +2.4 %; the unfused
+// engine with the prefetch is -2 %, so 0 is the default.
+#define IGM_POP_FUSED 0
+#endif
+constexpr bool kPopFused = IGM_POP_FUSED != 0;
 constexpr int kPopListRow = kPopListCap + 2;  // u16 per LDS list row of the build (odd word stride)
 
 struct PopBuf {
@@ -1239,7 +1250,7 @@ struct PopArgs {
     uint16_t* bdeg;      // (B, ldn)
     int bdmax;
     int kq;              // list quads per slot (4 kq >= the Verlet-list capacity)
-    int* flag;           // (B) list rebuild needed
+    int* flag[2];        // (B) list rebuild needed, by step parity (the force kernel clears the next step's)
     int* flist;          // (B) the flagged structures of this step, compacted
     int* nflag;          // (1)
     int* nrebuild;       // (B)
@@ -1263,7 +1274,8 @@ __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float
     if (s >= A.cm.nstruct) return;
     if (lb == 0 && threadIdx.x == 0) *A.nflag = 0;
     if (a == 0) {
-        A.flag[s] = 1;
+        A.flag[0][s] = 1;  // the first step builds
+        A.flag[1][s] = 0;
         A.nrebuild[s] = 0;
         A.par[s] = 0;
     }
@@ -1300,6 +1312,7 @@ struct PopStep {
     int rescale;      // apply the temp/rescale of step `prev` first
     int prev, nsteps;
     float t0, t1, window, fraction;
+    int fp;           // parity of this step's rebuild flags
 };
 
 // temp/rescale factor of structure s at the end of step P.prev (fixed-order sum of partials)
@@ -1368,7 +1381,7 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
         for (int d = 0; d < 6; ++d) red[(threadIdx.x >> 6) * 6 + d] = mm[d];
-    if (__syncthreads_or(moved) && threadIdx.x == 0) atomicOr(&A.flag[s], 1);
+    if (__syncthreads_or(moved) && threadIdx.x == 0) atomicOr(&A.flag[S.fp][s], 1);
     if (threadIdx.x < 6) {
         float m = red[threadIdx.x];
 #pragma unroll
@@ -1389,13 +1402,13 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
 // the sort is one workgroup's chain of dependent memory round trips, so fewer and
 // wider trips are what makes it faster.
 template <bool IDS_LDS, int APT>
-__global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A) {
+__global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cw[];  // (kPopCells + 1) / 2 words, then ids
     __shared__ int wsum[kMaxWaves];
     __shared__ float sg[6];
     __shared__ int sn[3];
     const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (!A.flag[s]) return;
+    if (!A.flag[fp][s]) return;
     const int N = A.cm.natom;
     const size_t base = (size_t)s * A.cm.ldn;
     const int p = A.par[s], q = p ^ 1;
@@ -1604,7 +1617,9 @@ __device__ __forceinline__ bool pop_build_slot(const PopArgs& A, int* s, int* i)
     return *i < A.cm.natom;
 }
 
-// state and bonds of every slot of a flagged structure into its new slot order
+// state (and with BONDS the bonds; the fused force kernel re-indexes them itself) of
+// every slot of a flagged structure into its new slot order
+template <bool BONDS>
 __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     int s, i;
     if (!pop_build_slot(A, &s, &i)) return;
@@ -1618,6 +1633,7 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     B.vel[k] = O.vel[o];
     // (no force: the force kernel of this step rewrites every slot's before any read)
     A.xb[k] = make_float4(x.x, x.y, x.z, 0.f);
+    if (!BONDS) return;
     // the atom's bonds (sorted adjacency of prepare()) with partners as slots
     const Bonds& Bd = A.cm.bonds;
     const int nsl = A.cm.nslice;
@@ -1667,81 +1683,95 @@ __device__ __forceinline__ float4 pop_ld(__amdgpu_buffer_rsrc_t r, uint32_t j) {
 // beat 2 and 6.  Staging positions in LDS does not pay, neither the block's whole
 // neighbourhood range (~50 KB, 18 % slower) nor the union of the slots its lists use
 // (lists rewritten to union indices: this kernel +58 %, the force kernel +9 %).
-__global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
-    __shared__ uint32_t lrow[kPopBS * kPopListRow / 2];
-    const int kb = blockIdx.x / A.nbs;
-    if (kb >= *A.nflag) return;  // an idle block (the structure was not flagged)
-    const int s = A.flist[kb], blk = blockIdx.x % A.nbs, t = threadIdx.x, i = blk * kPopBS + t;
-    const bool live = i < A.cm.natom;
-    const size_t base = (size_t)s * A.cm.ldn;
-    const float4* pos = A.buf[A.par[s]].pos + base;
-    const float4 p0 = pos[live ? i : 0];
-    const bool bead = live && p0.w >= 0.0f;
+// The Verlet list of bead slot i of structure s (p0 its position): collected in the
+// thread's LDS row `row` (kPopListRow u16), padded to whole quads with the slot itself,
+// stored as quads to the global list and its length (or kNnbWalk) to nnb.  Returns
+// the number of entries (> kcap: the slot takes its pairs from the cell walk).
+__device__ __forceinline__ int pop_fill_slot(const PopArgs& A, int s, int i, size_t base, const float4* pos,
+                                             float4 p0, uint32_t* row) {
     const float* gp = A.gp + (size_t)s * 8;
     const int* gn = A.gn + (size_t)s * 8;
     const int* cell = A.cell + (size_t)s * kPopCells;
     const int nx = gn[0], ny = gn[1], nz = gn[2];
     const int kcap = 4 * A.kq;  // <= kPopListCap
-    // The list is collected in this thread's LDS row (one u16 store per entry), then
-    // copied out a quad at a time: entry k of the slot is u16 k & 3 of quad k >> 2, the
-    // quads of a slice's 64 slots interleaved (coalesced uint2 stores).
-    uint16_t* lst = reinterpret_cast<uint16_t*>(lrow) + t * kPopListRow;
+    uint16_t* lst = reinterpret_cast<uint16_t*>(row);
     const float cut2 = A.P.cut_list * A.P.cut_list;
     int k = 0;
-    if (bead) {
-        // The 27 cells are 9 x-runs of slots.  All 18 run bounds are loaded together,
-        // then each z-layer's 3 runs a batch of kFillW slots per run at once (the rare
-        // longer run finishes in a loop): 4 dependent memory round trips per slot in
-        // place of one per run and per batch.
-        const int c = cell_index<float>(p0.x, p0.y, p0.z, gp, gp + 3, gn);
-        const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
-        const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
-        int rb[9], re[9];
+    // The 27 cells are 9 x-runs of slots.  All 18 run bounds are loaded together,
+    // then each z-layer's 3 runs a batch of kFillW slots per run at once (the rare
+    // longer run finishes in a loop): 4 dependent memory round trips per slot in
+    // place of one per run and per batch.
+    const int c = cell_index<float>(p0.x, p0.y, p0.z, gp, gp + 3, gn);
+    const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
+    const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
+    int rb[9], re[9];
 #pragma unroll
-        for (int r = 0; r < 9; ++r) {
-            const int z0 = cz + r / 3 - 1, y0 = cy + r % 3 - 1;
-            const bool ok = z0 >= 0 && z0 < nz && y0 >= 0 && y0 < ny;
-            const int row = ok ? (z0 * ny + y0) * nx : 0;
-            rb[r] = ok ? cell[row + xlo] : 0;
-            re[r] = ok ? cell[row + xhi + 1] : 0;
-        }
-        const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
-        auto test = [&](int j, const float3& p) {
-            const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
-            const bool in = j != i && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
-            if (in && k < kcap) lst[k] = (uint16_t)j;
-            k += in ? 1 : 0;
-        };
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-            float3 pp[3][kFillW];
-            int jj[3][kFillW];
-#pragma unroll
-            for (int r = 0; r < 3; ++r)
-#pragma unroll
-                for (int u = 0; u < kFillW; ++u) {
-                    const int j = rb[3 * g + r] + u;
-                    jj[r][u] = j < re[3 * g + r] ? j : i;  // past the run: the slot itself (never listed)
-                    pp[r][u] = pop_ld3(rp, jj[r][u]);
-                }
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-#pragma unroll
-                for (int u = 0; u < kFillW; ++u) test(jj[r][u], pp[r][u]);
-                for (int j = rb[3 * g + r] + kFillW; j < re[3 * g + r]; ++j) test(j, pop_ld3(rp, j));
-            }
-        }
-        // the last quad padded with the slot itself: a zero-distance entry adds no force
-        for (int kk = k; kk < kcap && (kk & 3); ++kk) lst[kk] = (uint16_t)i;
+    for (int r = 0; r < 9; ++r) {
+        const int z0 = cz + r / 3 - 1, y0 = cy + r % 3 - 1;
+        const bool ok = z0 >= 0 && z0 < nz && y0 >= 0 && y0 < ny;
+        const int rw = ok ? (z0 * ny + y0) * nx : 0;
+        rb[r] = ok ? cell[rw + xlo] : 0;
+        re[r] = ok ? cell[rw + xhi + 1] : 0;
     }
-    const int nlist = bead && k <= kcap ? ((k + 3) & ~3) : 0;  // entries incl. the padding
+    const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
+    auto test = [&](int j, const float3& p) {
+        const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
+        const bool in = j != i && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
+        if (in && k < kcap) lst[k] = (uint16_t)j;
+        k += in ? 1 : 0;
+    };
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        float3 pp[3][kFillW];
+        int jj[3][kFillW];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int u = 0; u < kFillW; ++u) {
+                const int j = rb[3 * g + r] + u;
+                jj[r][u] = j < re[3 * g + r] ? j : i;  // past the run: the slot itself (never listed)
+                pp[r][u] = pop_ld3(rp, jj[r][u]);
+            }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+#pragma unroll
+            for (int u = 0; u < kFillW; ++u) test(jj[r][u], pp[r][u]);
+            for (int j = rb[3 * g + r] + kFillW; j < re[3 * g + r]; ++j) test(j, pop_ld3(rp, j));
+        }
+    }
+    // the last quad padded with the slot itself: a zero-distance entry adds no force
+    for (int kk = k; kk < kcap && (kk & 3); ++kk) lst[kk] = (uint16_t)i;
+    const int nlist = k <= kcap ? ((k + 3) & ~3) : 0;  // entries incl. the padding
     if (nlist > 0) {
         uint64_t* out = reinterpret_cast<uint64_t*>(A.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * A.kq * 64 + (i & 63));
-        const uint32_t* row = lrow + t * (kPopListRow / 2);
 #pragma unroll 1
         for (int q = 0; q < nlist >> 2; ++q) out[(size_t)q * 64] = ((uint64_t)row[2 * q + 1] << 32) | row[2 * q];
     }
-    if (live) A.nnb[base + i] = (uint16_t)(!bead ? 0 : (k <= kcap ? k : kNnbWalk));
+    A.nnb[base + i] = (uint16_t)(k <= kcap ? k : kNnbWalk);
+    return k;
+}
+
+// Verlet list of every bead slot of a flagged structure (the unfused engine): the 27
+// cells around its cell, each x-run of cells one contiguous slot range.  Measured on
+// config C (kernel traces, scripts/gpu_profab.sh): collecting the list in an LDS row
+// and storing it a quad at a time is 13 % faster than one global u16 store per entry;
+// batches of 4 slots per run beat 2 and 6.  Staging positions in LDS does not pay,
+// neither the block's whole neighbourhood range (~50 KB, 18 % slower) nor the union of
+// the slots its lists use (lists rewritten to union indices: this kernel +58 %, the
+// force kernel +9 %).
+__global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
+    __shared__ uint32_t lrow[kPopBS * kPopListRow / 2];
+    const int kb = blockIdx.x / A.nbs;
+    if (kb >= *A.nflag) return;  // an idle block (the structure was not flagged)
+    const int s = A.flist[kb], blk = blockIdx.x % A.nbs, t = threadIdx.x, i = blk * kPopBS + t;
+    if (i >= A.cm.natom) return;
+    const size_t base = (size_t)s * A.cm.ldn;
+    const float4* pos = A.buf[A.par[s]].pos + base;
+    const float4 p0 = pos[i];
+    if (p0.w >= 0.0f)
+        pop_fill_slot(A, s, i, base, pos, p0, lrow + t * (kPopListRow / 2));
+    else
+        A.nnb[base + i] = 0;
 }
 
 // pair forces of a slot past the Verlet-list capacity: the 27 cells of the build-time
@@ -1767,21 +1797,48 @@ __device__ __noinline__ float4 pop_walk_pairs(const float4* pos, const int* cell
 // place of the IEEE sqrt/divide expansions, no calls (a call would put the kernel
 // arguments in scratch).  Neighbours and bond partners are loaded a batch at a time
 // so their gathers are in flight together; a masked tail keeps the batch branch-free.
+//   Fused rebuild step (lrow != null): the slot's list was just built into its LDS row
+// (nn_built entries) and is read from there; the slot's bonds are re-indexed from the
+// atom-space adjacency into the new slot order here (written to bent/bdeg for the
+// following steps) and used directly.
 __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, size_t base, const float4* pos,
                                                uint32_t fl, float evf, float envf, float& fx, float& fy,
-                                               float& fz) {
+                                               float& fz, const uint32_t* lrow = nullptr, int nn_built = 0) {
     constexpr int U = kPopPairBatch;  // list quads per batch
     const int nsl = A.cm.nslice;
     const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
-    const uint32_t* g = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
+    uint32_t* g = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
     const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
     const float4 p0 = pos[i];
     const float xi = p0.x, yi = p0.y, zi = p0.z, ri = p0.w;
     fx = fy = fz = 0.0f;
     const float evfpi = evf * 0.318309886183790671537767526745f;
-    const int nn = A.nnb[base + i];
-    const int deg = A.bdeg[base + i];
+    const bool rebuilt = lrow != nullptr;
+    const int nn = rebuilt ? (nn_built <= 4 * A.kq ? nn_built : kNnbWalk) : A.nnb[base + i];
+    const int* sl = A.buf[A.par[s]].slot + base;
+    int a_id = 0;
+    const uint32_t* ga = nullptr;  // atom-space adjacency (rebuilt step)
+    int deg;
+    if (rebuilt) {
+        const Bonds& Bd = A.cm.bonds;
+        a_id = A.buf[A.par[s]].aid[base + i];
+        deg = Bd.deg[(size_t)s * A.cm.natom + a_id];
+        ga = Bd.ent + Bd.base[s] + Bd.soff[(size_t)s * (nsl + 1) + (a_id >> 6)] + (a_id & 63);
+        A.bdeg[base + i] = (uint16_t)deg;
+    } else {
+        deg = A.bdeg[base + i];
+    }
+#if IGM_POP_PREFETCH
+    // Latency: the slot's loads, its first list quad and first bond entries go out in
+    // one memory round trip (their addresses depend on (s, i) only; slots past the
+    // atom's own are clamped into the allocated region and never used).
+    uint2 qnext = make_uint2(i * 0x10001u, i * 0x10001u);
+    if (!rebuilt) qnext = gl[0];
+    uint32_t et0[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) et0[u] = rebuilt ? 0u : g[(size_t)min(u, A.bdmax - 1) * 64];
+#endif
     // Two list entries per packed-f32 op.  With t = 1/(r rc) from ONE rsq,
     //   sin(pi r / rc) = sin_rev(r2 t / 2)   and   evf rc sin / (pi r) = evfpi rc2 t sin,
     // the soft_pair_bf force without the rcp; the 1e-20 keeps a zero distance (the
@@ -1826,11 +1883,25 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         } else {
             const int nq = (nn + 3) >> 2;
             auto pairs = [&](auto fetch) {
+#if IGM_POP_PREFETCH
+                // one quad at a time, the next quad's load in flight with this one's gathers
+                for (int q = 0; q < nq; ++q) {
+                    const uint2 e = rebuilt ? make_uint2(lrow[2 * q], lrow[2 * q + 1]) : qnext;
+                    if (!rebuilt && q + 1 < nq) qnext = gl[(size_t)(q + 1) * 64];
+                    const float4 a0 = fetch(e.x & 0xffffu), a1 = fetch(e.x >> 16), a2 = fetch(e.y & 0xffffu),
+                                 a3 = fetch(e.y >> 16);
+                    pair2(a0, a1);
+                    pair2(a2, a3);
+                }
+                return;
+#endif
                 for (int q0 = 0; q0 < nq; q0 += U) {
                     uint2 e[U];  // a quad past the list: the slot itself 4 times (no force)
 #pragma unroll
                     for (int u = 0; u < U; ++u)
-                        e[u] = q0 + u < nq ? gl[(size_t)(q0 + u) * 64] : make_uint2(i * 0x10001u, i * 0x10001u);
+                        e[u] = q0 + u >= nq ? make_uint2(i * 0x10001u, i * 0x10001u)
+                               : rebuilt    ? make_uint2(lrow[2 * (q0 + u)], lrow[2 * (q0 + u) + 1])
+                                            : gl[(size_t)(q0 + u) * 64];
                     float4 pt[4 * U];
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -1872,8 +1943,27 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 #endif
     for (int k0 = 0; k0 < deg; k0 += 4) {
         uint32_t et[4];
+        if (rebuilt) {  // atom-space entries -> slot-space (the permute of the unfused engine)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) et[u] = g[(size_t)min(k0 + u, deg - 1) * 64];
+            for (int u = 0; u < 4; ++u) et[u] = ga[(size_t)min(k0 + u, deg - 1) * 64];
+            int sv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sv[u] = sl[et[u] & 0xffffu];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                et[u] = (et[u] & 0xffff0000u) | (uint32_t)sv[u];
+                if (k0 + u < deg) g[(size_t)(k0 + u) * 64] = et[u];
+            }
+        } else {
+#if IGM_POP_PREFETCH
+            if (k0 == 0) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) et[u] = u < deg ? et0[u] : et0[0];  // (past deg: a valid entry)
+            } else
+#endif
+#pragma unroll
+            for (int u = 0; u < 4; ++u) et[u] = g[(size_t)min(k0 + u, deg - 1) * 64];
+        }
         float4 pt[4];
         float2 ct[4];
 #pragma unroll
@@ -1932,14 +2022,23 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 // when S.integrate; the run's setup evaluation otherwise).  (Measured on config C: a
 // block running the pairs and the bonds of its slots in separate waves at the same
 // time is 6 % slower than one thread per slot doing both.)
+//   FUSED: a structure whose list is rebuilt this step builds it here, a slot per
+// thread (pop_fill_slot into the thread's LDS row), and takes this step's pairs from
+// that row and its bonds from the atom-space adjacency (pop_slot_force's rebuilt
+// path): no fill launch, no list or bond re-read on rebuild steps.  Every cross-slot
+// input (the new slot order, cell offsets and positions) was written by the sort and
+// permute kernels before this launch.
+template <bool FUSED>
 __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(PopArgs A, float evf, float envf, PopStep S) {
     __shared__ double red[kPopBS / 64];
+    __shared__ uint32_t lrow[FUSED ? kPopBS * kPopListRow / 2 : 1];
     const int lb = pop_block(), s = lb / A.nbs, blk = lb % A.nbs, i = blk * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
     if (lb == 0 && threadIdx.x == 0) *A.nflag = 0;  // the build kernels of this step are done
-    if (i == 0 && A.flag[s]) {  // the structure's list was rebuilt this step
-        A.flag[s] = 0;
-        A.nrebuild[s] += 1;
+    const int rebuilt = A.flag[S.fp][s];  // the structure's list is (was) rebuilt this step
+    if (i == 0) {
+        A.nrebuild[s] += rebuilt ? 1 : 0;
+        A.flag[S.fp ^ 1][s] = 0;  // the next step's flags start clear
     }
     const size_t base = (size_t)s * A.cm.ldn, k = base + i;
     const PopBuf& B = A.buf[A.par[s]];
@@ -1948,7 +2047,18 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
         float4 v = B.vel[k];
         const uint32_t fl = __float_as_uint(v.w);
         float fx, fy, fz;
-        pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz);
+        if (FUSED && rebuilt) {
+            uint32_t* row = lrow + threadIdx.x * (kPopListRow / 2);
+            const float4 p0 = B.pos[k];
+            int nb = 0;
+            if (p0.w >= 0.0f)
+                nb = pop_fill_slot(A, s, i, base, B.pos + base, p0, row);
+            else
+                A.nnb[k] = 0;
+            pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, row, nb);
+        } else {
+            pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz);
+        }
         B.frc[k] = make_float4(fx, fy, fz, 0.f);
         if (S.integrate && !(fl & IGM_ATOM_FIXED)) {
             kick_limit(v.x, v.y, v.z, fx, fy, fz, S.dtf, S.vlim, S.vlimsq);
@@ -2983,7 +3093,8 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     V.gn = Q.gn + (size_t)s0 * 8;
     V.bent = Q.bent + (size_t)s0 * nsl * Q.bdmax * 64;
     V.bdeg = Q.bdeg + o;
-    V.flag = Q.flag + s0;
+    V.flag[0] = Q.flag[0] + s0;
+    V.flag[1] = Q.flag[1] + s0;
     V.flist = Q.flist + s0;
     V.nflag = Q.nflag + g;
     V.nrebuild = Q.nrebuild + s0;
@@ -3035,7 +3146,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     IGM_TRY(workspace(c, "pop_gn", sizeof(int) * 8 * (size_t)S, &pgn));
     IGM_TRY(workspace(c, "pop_bent", sizeof(uint32_t) * SL * Q.bdmax, &pbent));
     IGM_TRY(workspace(c, "pop_bdeg", sizeof(uint16_t) * SL, &pbdeg));
-    IGM_TRY(workspace(c, "pop_flag", sizeof(int) * (size_t)S, &pfl));
+    IGM_TRY(workspace(c, "pop_flag", sizeof(int) * 2 * (size_t)S, &pfl));
     IGM_TRY(workspace(c, "pop_flist", sizeof(int) * (size_t)S, &pfli));
     IGM_TRY(workspace(c, "pop_nflag", sizeof(int) * 64, &pnf));
     IGM_TRY(workspace(c, "pop_ke", sizeof(double) * (size_t)S * Q.nbs, &pke));
@@ -3051,7 +3162,8 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.gn = (int*)pgn;
     Q.bent = (uint32_t*)pbent;
     Q.bdeg = (uint16_t*)pbdeg;
-    Q.flag = (int*)pfl;
+    Q.flag[0] = (int*)pfl;
+    Q.flag[1] = (int*)pfl + S;
     Q.flist = (int*)pfli;
     Q.nflag = (int*)pnf;
     Q.kep = (double*)pke;
@@ -3119,6 +3231,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                                A.vel + g0[g] * n3, A.forces_out ? A.forces_out + g0[g] * n3 : nullptr);
         }
     }
+    long gbase = 0;  // steps of the earlier segments: the flag parity runs on across segments
     for (int seg = 0; seg < A.nseg; ++seg) {
         const float* vsrc = A.mode == 1 ? A.vel : A.vinit + (size_t)seg * n3;
         const size_t sstride = A.mode == 1 ? n3 : (size_t)A.nseg * n3;
@@ -3146,19 +3259,21 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                     st.integrate = step > 0;
                     st.rescale = step > 1;
                     st.prev = step - 1;
+                    st.fp = (int)((gbase + step) & 1);
                     for (int g = w0; g < w0 + nc && g < ng; ++g) {
                         const int ns = g0[g + 1] - g0[g];
                         hipStream_t sg = strm(g);
                         hipLaunchKernelGGL(pop_integrate_kernel, grid_of(g), blk, 0, sg, V[g], st);
-                        hipLaunchKernelGGL(sort_kern, dim3(ns), dim3(kPopSortNT), sort_lds, sg, V[g]);
-                        hipLaunchKernelGGL(pop_permute_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
-                        hipLaunchKernelGGL(pop_fill_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
-                        hipLaunchKernelGGL(pop_force_kernel, grid_of(g), blk, 0, sg, V[g], evf, envf, st);
+                        hipLaunchKernelGGL(sort_kern, dim3(ns), dim3(kPopSortNT), sort_lds, sg, V[g], st.fp);
+                        hipLaunchKernelGGL(pop_permute_kernel<!kPopFused>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                        if (!kPopFused) hipLaunchKernelGGL(pop_fill_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                        hipLaunchKernelGGL(pop_force_kernel<kPopFused>, grid_of(g), blk, 0, sg, V[g], evf, envf, st);
                     }
                 }
             }
         }
         IGM_HIP_CHECK(c, hipGetLastError());
+        gbase += st.nsteps + 1;
         st.rescale = st.nsteps > 0;
         st.prev = st.nsteps;
         const bool last = seg + 1 == A.nseg;
