@@ -311,6 +311,20 @@ def measured_traffic(config):
     return float(d['fetch_bytes_per_launch']) + float(d['write_bytes_per_launch']), d['source']
 
 
+def measured_issue(config):
+    """VALU-issue roofline of the anneal kernel from the committed SQ counter passes
+    (scripts/gpu_r02.sh -> profiles/<round>/sq*.txt), kept in bench_issue.json: the
+    fraction of each SIMD's cycles spent issuing VALU instructions (a wave64 VALU op
+    occupies a 16-lane SIMD for 4 cycles): SQ_INSTS_VALU * SQ_WAVES / (SIMDs *
+    SQ_WAVE_CYCLES) with every wave resident for the whole launch.  The anneal kernel
+    keeps its structure in LDS, so this -- not HBM -- is its binding roofline."""
+    path = os.path.join(ROOT, 'bench_issue.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        return json.load(fh).get(config)
+
+
 def main():
     args = parse()
     import torch
@@ -399,6 +413,7 @@ def main():
                          'traffic_source': traffic_src,
                          'algorithmic_bytes_per_launch': float(np.mean(bytes_launch)),
                          'avg_launch_ms': a_ms},
+            'roofline_issue': measured_issue(args.config),
             'cpu_baseline': cpu,
             'cpu_baseline_astep': astep_cpu,
             'astep_pairs_per_s': float(it.npairs) / (kms['actdist'] * 1e-3),

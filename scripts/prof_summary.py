@@ -33,6 +33,28 @@ def kernel_stats(db):
     return lines
 
 
+def busy_union(db, pattern='pop_'):
+    """GPU-busy share of the kernels matching `pattern`: the union of their [start, end)
+    intervals over the span from the first start to the last end, and the mean number
+    of them running at once (sum of durations / union)."""
+    c = sqlite3.connect(db)
+    iv = sorted(c.execute('select start, end from kernels where name like ?', ('%' + pattern + '%',)))
+    if not iv:
+        return None
+    union, cur_s, cur_e, tot = 0, iv[0][0], iv[0][1], 0
+    for a, b in iv:
+        tot += b - a
+        if a > cur_e:
+            union += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    union += cur_e - cur_s
+    span = max(b for _, b in iv) - iv[0][0]
+    return {'span_ms': span * 1e-6, 'busy_ms': union * 1e-6, 'busy_frac': union / span,
+            'mean_concurrency': tot / union, 'launches': len(iv)}
+
+
 def pmc(db):
     c = sqlite3.connect(db)
     q = ('select kernel_name, counter_name, count(*), sum(value), avg(end - start) from counters_collection '
@@ -46,6 +68,10 @@ def main(src, dst):
         with open(os.path.join(dst, 'kernel_stats.txt'), 'w') as f:
             f.write('# rocprofv3 --kernel-trace --stats, %s\n' % os.path.basename(db))
             f.write('\n'.join(kernel_stats(db)) + '\n')
+            for pat in ('pop_', 'anneal_kernel'):
+                u = busy_union(db, pat)
+                if u:
+                    f.write('# busy union of %s kernels: %s\n' % (pat, u))
     out = ['# PMC passes (one counter per rocprofv3 run). value_KB = rocprofv3 FETCH_SIZE/WRITE_SIZE summed over',
            '# the launches; hbm_bytes_per_launch = KB*1024/calls, FETCH_SIZE doubled (gfx950 correction).',
            '%-70s %-10s %6s %18s %22s %14s' % ('kernel', 'counter', 'calls', 'value_KB', 'hbm_bytes_per_launch',
