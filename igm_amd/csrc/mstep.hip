@@ -1258,6 +1258,12 @@ struct PopArgs {
     float* bbp;          // (B, nbs, 6) per-block bounding boxes {max -x, -y, -z, max x, y, z}
     const double* dofs;  // (B) dof of group nonfixed
     int nbs;
+    // the bonds of every atom as contiguous rows (CSR, the sliced ELLPACK of prepare()
+    // re-laid out once per run): the rebuild's re-index gathers atoms in slot order,
+    // where one row is one cache line instead of one line per entry
+    const uint32_t* csr;  // entries: partner atom | type << 16 | lower << 31
+    const int* coff;      // (B, natom + 1) row offsets within the structure
+    const int64_t* cbase;  // (B) first entry of the structure
 };
 
 // XCD-aware block order for the kernels over every structure: the grid (padded to a
@@ -1267,6 +1273,26 @@ struct PopArgs {
 __device__ __forceinline__ int pop_block() {
     const int x = blockIdx.x, per = gridDim.x >> 3;
     return (x & 7) * per + (x >> 3);
+}
+
+// CSR row offsets of every structure's bonds (one workgroup per structure): the
+// exclusive scan of the atom degrees, the structure's total at coff[natom]
+__global__ void __launch_bounds__(1024) pop_csr_scan_kernel(const int* deg, int natom, int* coff) {
+    __shared__ int wsum[1024 / 64];
+    const int s = blockIdx.x;
+    block_scan<1024, int, int>(deg + (size_t)s * natom, coff + (size_t)s * (natom + 1), natom, wsum);
+}
+
+// the entries of every atom's row from the sliced ELLPACK adjacency
+__global__ void __launch_bounds__(256) pop_csr_fill_kernel(Bonds Bd, int nstruct, int natom, int nslice,
+                                                            const int* coff, const int64_t* cbase, uint32_t* csr) {
+    const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (x >= (int64_t)nstruct * natom) return;
+    const int s = (int)(x / natom), a = (int)(x - (int64_t)s * natom);
+    const int deg = Bd.deg[x];
+    const uint32_t* g = Bd.ent + Bd.base[s] + Bd.soff[(size_t)s * (nslice + 1) + (a >> 6)] + (a & 63);
+    uint32_t* o = csr + cbase[s] + coff[(size_t)s * (natom + 1) + a];
+    for (int e = 0; e < deg; ++e) o[e] = g[(size_t)e * 64];
 }
 
 __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float* xyz) {
@@ -1635,17 +1661,17 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     A.xb[k] = make_float4(x.x, x.y, x.z, 0.f);
     if (!BONDS) return;
     // the atom's bonds (sorted adjacency of prepare()) with partners as slots
-    const Bonds& Bd = A.cm.bonds;
     const int nsl = A.cm.nslice;
-    const int deg = Bd.deg[(size_t)s * A.cm.natom + a];
-    const uint32_t* g = Bd.ent + Bd.base[s] + Bd.soff[(size_t)s * (nsl + 1) + (a >> 6)] + (a & 63);
+    const int* co = A.coff + (size_t)s * (A.cm.natom + 1);
+    const int r0 = co[a], deg = co[a + 1] - r0;
+    const uint32_t* g = A.csr + A.cbase[s] + r0;
     uint32_t* d = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const int* sl = B.slot + base;
     for (int e0 = 0; e0 < deg; e0 += 4) {  // 4 entries, then their 4 slots, in flight together
         uint32_t v[4];
         int t[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = g[(size_t)min(e0 + u, deg - 1) * 64];
+        for (int u = 0; u < 4; ++u) v[u] = g[min(e0 + u, deg - 1)];
 #pragma unroll
         for (int u = 0; u < 4; ++u) t[u] = sl[v[u] & 0xffffu];
 #pragma unroll
@@ -1821,10 +1847,11 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     const uint32_t* ga = nullptr;  // atom-space adjacency (rebuilt step)
     int deg;
     if (rebuilt) {
-        const Bonds& Bd = A.cm.bonds;
         a_id = A.buf[A.par[s]].aid[base + i];
-        deg = Bd.deg[(size_t)s * A.cm.natom + a_id];
-        ga = Bd.ent + Bd.base[s] + Bd.soff[(size_t)s * (nsl + 1) + (a_id >> 6)] + (a_id & 63);
+        const int* co = A.coff + (size_t)s * (A.cm.natom + 1);
+        const int r0 = co[a_id];
+        deg = co[a_id + 1] - r0;
+        ga = A.csr + A.cbase[s] + r0;
         A.bdeg[base + i] = (uint16_t)deg;
     } else {
         deg = A.bdeg[base + i];
@@ -1945,7 +1972,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         uint32_t et[4];
         if (rebuilt) {  // atom-space entries -> slot-space (the permute of the unfused engine)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) et[u] = ga[(size_t)min(k0 + u, deg - 1) * 64];
+            for (int u = 0; u < 4; ++u) et[u] = ga[min(k0 + u, deg - 1)];
             int sv[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) sv[u] = sl[et[u] & 0xffffu];
@@ -3101,6 +3128,8 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     V.kep = Q.kep + (size_t)s0 * Q.nbs;
     V.bbp = Q.bbp + (size_t)s0 * Q.nbs * 6;
     V.dofs = Q.dofs + s0;
+    V.coff = Q.coff + (size_t)s0 * (Q.cm.natom + 1);
+    V.cbase = Q.cbase + s0;
     return V;
 }
 
@@ -3189,6 +3218,33 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         IGM_HIP_CHECK(c, hipMemcpyAsync(pdof, dofs.data(), sizeof(double) * S, hipMemcpyHostToDevice, c->stream));
         IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
         Q.dofs = (const double*)pdof;
+    }
+    // bond rows as CSR (per-structure offsets by a block scan, structure bases on the host)
+    {
+        void *pco, *pcb, *pcsr;
+        IGM_TRY(workspace(c, "pop_coff", sizeof(int) * (size_t)S * (N + 1), &pco));
+        hipLaunchKernelGGL(pop_csr_scan_kernel, dim3(S), dim3(1024), 0, c->stream, pr.cm.bonds.deg, N, (int*)pco);
+        std::vector<int> tot(S);
+        IGM_HIP_CHECK(c, hipMemcpy2DAsync(tot.data(), sizeof(int), (const int*)pco + N, sizeof(int) * (N + 1),
+                                          sizeof(int), S, hipMemcpyDeviceToHost, c->stream));
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+        std::vector<int64_t> cb(S);
+        int64_t run = 0;
+        for (int st = 0; st < S; ++st) {
+            cb[st] = run;
+            run += tot[st];
+        }
+        IGM_TRY(workspace(c, "pop_cbase", sizeof(int64_t) * (size_t)S, &pcb));
+        IGM_TRY(workspace(c, "pop_csr", sizeof(uint32_t) * (size_t)(run > 0 ? run : 1), &pcsr));
+        IGM_HIP_CHECK(c, hipMemcpyAsync(pcb, cb.data(), sizeof(int64_t) * S, hipMemcpyHostToDevice, c->stream));
+        const int64_t nx = (int64_t)S * N;
+        hipLaunchKernelGGL(pop_csr_fill_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, c->stream,
+                           pr.cm.bonds, S, N, pr.cm.nslice, (const int*)pco, (const int64_t*)pcb, (uint32_t*)pcsr);
+        IGM_HIP_CHECK(c, hipGetLastError());
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));  // cb (host) must outlive the copy
+        Q.coff = (const int*)pco;
+        Q.cbase = (const int64_t*)pcb;
+        Q.csr = (const uint32_t*)pcsr;
     }
     // the sort keeps its ids in LDS when they fit beside the cell counts (200 kb: 29 839 atoms)
     const bool ids_lds = pop_sort_lds(true, N) <= kLdsBytes;
