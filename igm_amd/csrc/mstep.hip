@@ -294,6 +294,9 @@ __device__ __forceinline__ int cell_index(T x, T y, T z, const T* lo, const T* i
 #ifndef IGM_WALK_BATCH
 #define IGM_WALK_BATCH 4
 #endif
+#ifndef IGM_WALK_SORTED
+#define IGM_WALK_SORTED 1  // LDS list build: threads walk the beads in cell order
+#endif
 template <int WB = IGM_WALK_BATCH, typename OffT, typename F>
 __device__ __forceinline__ void walk27(int c, const OffT* cell, const uint16_t* sorted, const int* gn, F&& f) {
     const int nx = gn[0], ny = gn[1], nz = gn[2];
@@ -608,7 +611,18 @@ __device__ __noinline__ unsigned long long build_nlist_lds(int natom, const floa
     // one pass: walk the 27 cells (9 x-runs of consecutive sorted slots), write the
     // list slots (the count scratch above is dead)
     const int nx = nb[0], ny = nb[1], nz = nb[2];
+#if IGM_WALK_SORTED
+    // threads take the beads in cell order (lanes of a wave = neighbouring cells: their
+    // 27-cell walks have similar run lengths and read neighbouring positions); the
+    // non-bead atoms have empty lists
+    for (int a = t; a < natom; a += NT)
+        if (!(lds_f4(pos, a).w >= 0.0f)) nnb[a] = 0;
+    const int nsorted = (int)cell[ncell];
+    for (int qa = t; qa < nsorted; qa += NT) {
+        const int a = (int)sorted[qa];
+#else
     for (int a = t; a < natom; a += NT) {
+#endif
         const float4 p0 = lds_f4(pos, a);
         int k = 0;
         if (p0.w >= 0.0f) {
