@@ -19,6 +19,10 @@
 //   vlen data: {length u32, global-heap collection address u64, object index u32};
 //     a collection ("GCOL", size >= 4096) holds objects {index u16, refcount u16,
 //     4 reserved, size u64, data padded to 8}, index 0 = the free space
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -137,8 +141,20 @@ struct Object {
 
 }  // namespace
 
+// the file's bytes: a read-only memory map (only the touched pages are read -- opening a
+// population file to read its index does not read its coordinates)
+struct FileBytes {
+    const uint8_t* p = nullptr;
+    size_t n = 0;
+    ~FileBytes() {
+        if (p) munmap(const_cast<uint8_t*>(p), n);
+    }
+    const uint8_t* data() const { return p; }
+    size_t size() const { return n; }
+};
+
 struct igm_h5 {
-    std::vector<uint8_t> buf;
+    FileBytes buf;
     uint64_t base = 0, root = kUndef;
     int leafk = 4, intk = 16;
     std::map<std::string, uint64_t> paths;  // resolved object headers
@@ -540,16 +556,24 @@ extern "C" const char* igm_io_last_error(void) { return g_err.c_str(); }
 extern "C" int igm_h5_open(const char* path, igm_h5** out) {
     if (!path || !out) return fail("igm_h5_open: null argument");
     *out = nullptr;
-    FILE* fp = fopen(path, "rb");
-    if (!fp) return fail("igm_h5_open: cannot open '%s'", path);
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return fail("igm_h5_open: cannot open '%s'", path);
     std::unique_ptr<igm_h5> f(new igm_h5());
-    fseek(fp, 0, SEEK_END);
-    const long n = ftell(fp);
-    fseek(fp, 0, SEEK_SET);
-    f->buf.resize(n > 0 ? (size_t)n : 0);
-    const size_t got = n > 0 ? fread(f->buf.data(), 1, (size_t)n, fp) : 0;
-    fclose(fp);
-    if ((long)got != n) return fail("igm_h5_open: short read of '%s'", path);
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        close(fd);
+        return fail("igm_h5_open: cannot stat '%s'", path);
+    }
+    if (st.st_size > 0) {
+        void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) {
+            close(fd);
+            return fail("igm_h5_open: cannot map '%s'", path);
+        }
+        f->buf.p = static_cast<const uint8_t*>(m);
+        f->buf.n = (size_t)st.st_size;
+    }
+    close(fd);
     try {
         // the superblock may sit at 0, 512, 1024, ... (a user block before it)
         size_t sb = kUndef;
