@@ -13,7 +13,7 @@ for r in $RUNS; do
     for kv in ${envs//,/ }; do export "$kv"; done
     [ -n "$lib" ] && export IGM_HIP_LIB=$PWD/igm_amd/lib/ab/libigmhip_$lib.so
     if [ "$cfg" = C ]; then sc=${SCALE_C:-0.1}; ns=${NSTRUCT_C:-125}; else sc=${SCALE_B:-0.2}; ns=${NSTRUCT_B:-1000}; fi
-    timeout -k 10 600 python -u bench.py --config $cfg --nstruct $ns --protocol-scale $sc --steps 1 --warmup 0 \
+    timeout -k 10 600 python -u bench.py --config $cfg --nstruct $ns --protocol-scale $sc --steps 1 --warmup ${WARMUP:-0} \
       --cpu-sample 0 --no-de --no-c > gpurun_out/tune_$(printf %02d $i)_$tag.log 2>&1
   )
   rc=$?; echo "$r rc=$rc"; [ $rc -eq 0 ] || exit $rc
