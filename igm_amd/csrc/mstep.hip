@@ -494,8 +494,7 @@ __device__ __noinline__ unsigned long long build_nlist_lds(int natom, const floa
     }
 #pragma unroll
     for (int d = 0; d < 6; ++d)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) mm[d] = fmaxf(mm[d], __shfl_xor(mm[d], off));
+        mm[d] = wave_max_f32(mm[d]);
     if (lane == 0)
 #pragma unroll
         for (int d = 0; d < 6; ++d) redf[w * 6 + d] = mm[d];
@@ -1368,8 +1367,7 @@ __device__ __forceinline__ float pop_factor(const PopArgs& A, const PopStep& S, 
         const double* kp = A.kep + (size_t)s * A.nbs;
         double ke = 0.0;
         for (int i = threadIdx.x; i < A.nbs; i += 64) ke += kp[i];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) ke += __shfl_xor(ke, off);
+        ke = wave_sum_f64(ke);
         if (threadIdx.x == 0)
             *shared = temp_rescale_factor(ke, A.dofs[s], S.prev, S.nsteps, S.t0, S.t1, S.window, S.fraction);
     }
@@ -1421,8 +1419,7 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     // this block's bounding box of the beads (for a list build of the structure)
 #pragma unroll
     for (int d = 0; d < 6; ++d)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) mm[d] = fmaxf(mm[d], __shfl_xor(mm[d], off));
+        mm[d] = wave_max_f32(mm[d]);
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
         for (int d = 0; d < 6; ++d) red[(threadIdx.x >> 6) * 6 + d] = mm[d];
@@ -1466,8 +1463,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
         const float* bp = A.bbp + (size_t)s * A.nbs * 6;
         float m = -3.0e38f;
         for (int b = lane; b < A.nbs; b += 64) m = fmaxf(m, bp[b * 6 + w]);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        m = wave_max_f32(m);
         if (lane == 0) smm[w] = m;
     }
     __syncthreads();
@@ -2113,8 +2109,7 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
         }
     }
     if (!S.integrate) return;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) ke += __shfl_xor(ke, off);
+    ke = wave_sum_f64(ke);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ke;
     __syncthreads();
     if (threadIdx.x == 0) {

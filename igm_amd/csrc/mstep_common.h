@@ -58,6 +58,60 @@ struct DevParams {
 };
 
 // ------------------------------------------------------------- reductions
+#ifndef IGM_DPP_REDUCE
+#define IGM_DPP_REDUCE 1
+#endif
+// a double moved across lanes by one DPP control (both halves, full row/bank masks)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Sum of a double over the 64 lanes, the same bits in every lane.  DPP inside each
+// 16-lane row (quad xor 1, quad xor 2, half-row mirror, row mirror: every lane of a
+// row then holds the row sum, addition being commutative), then the four row sums
+// through readlane -- no LDS-crossbar round trips (ds_bpermute) on the chain.
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#if IGM_DPP_REDUCE
+    v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);  // row_half_mirror
+    v += dpp_f64<0x140>(v);  // row_mirror
+    return ((readlane_f64(v, 0) + readlane_f64(v, 16)) + readlane_f64(v, 32)) + readlane_f64(v, 48);
+#else
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+#endif
+}
+
+// max of a float over the 64 lanes, every lane (exact: the same bits in any order)
+__device__ __forceinline__ float wave_max_f32(float v) {
+#if IGM_DPP_REDUCE
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xf, 0xf, false)));
+    const float a = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)),
+                          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16)));
+    const float b = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
+                          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
+    return fmaxf(a, b);
+#else
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+#endif
+}
+
 // Sum K doubles over the block.  Only lane 0 of each wave publishes; every
 // thread then adds the per-wave partials in the same order, so all threads get
 // the bitwise identical result (uniform control flow afterwards).  `red` must
@@ -66,9 +120,7 @@ struct DevParams {
 template <int NT, int K>
 __device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    for (int k = 0; k < K; ++k) v[k] = wave_sum_f64(v[k]);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0)
 #pragma unroll
