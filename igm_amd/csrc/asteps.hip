@@ -1201,6 +1201,14 @@ extern "C" int igm_contact_map_haploid(igm_ctx* c, uint32_t flags, const float* 
     // the haploid locus of every bead from the CSR copy index (host pointers)
     std::vector<int32_t> hap(nbead, -1);
     if (copy_ptr[0] != 0) return fail(c, IGM_E_INVALID, "igm_contact_map_haploid: copy_ptr[0] != 0");
+    // every bead belongs to exactly one haploid locus, so copy_idx holds nbead entries:
+    // a non-decreasing copy_ptr ending at nbead keeps every read inside it
+    for (int a = 0; a < nhap; ++a)
+        if (copy_ptr[a + 1] < copy_ptr[a] || copy_ptr[a + 1] > nbead)
+            return fail(c, IGM_E_INVALID, "igm_contact_map_haploid: copy_ptr not non-decreasing within [0, %d]", nbead);
+    if (copy_ptr[nhap] != nbead)
+        return fail(c, IGM_E_INVALID, "igm_contact_map_haploid: copy_ptr[%d] = %d, expected nbead = %d", nhap,
+                    copy_ptr[nhap], nbead);
     for (int a = 0; a < nhap; ++a)
         for (int k = copy_ptr[a]; k < copy_ptr[a + 1]; ++k) {
             const int b = copy_idx[k];

@@ -244,6 +244,9 @@ struct igm_h5 {
         s.nelem = 1;
         for (int d = 0; d < s.rank; ++d) {
             s.dims[d] = (int64_t)rd(p + o + 8 * d, 8);
+            // a corrupt extent must not turn into a huge (or negative) allocation
+            if (s.dims[d] < 0 || (s.dims[d] > 0 && s.nelem > ((int64_t)1 << 48) / s.dims[d]))
+                raise("HDF5: implausible dataspace extent %lld in dimension %d", (long long)s.dims[d], d);
             s.nelem *= s.dims[d];
         }
         return s;
@@ -266,16 +269,24 @@ struct igm_h5 {
                 case 0x08: {
                     if (m.n < 2 || m.p[0] != 3) raise("HDF5: data layout version %d is not supported", m.n ? m.p[0] : -1);
                     ob.lay.cls = m.p[1];
+                    // every field is checked against the message size before it is read
+                    auto need = [&](size_t k) {
+                        if (k > m.n) raise("HDF5: data layout message too short (%zu of %zu bytes)", (size_t)m.n, k);
+                    };
                     if (ob.lay.cls == 0) {
+                        need(4);
                         ob.lay.size = rd(m.p + 2, 2);
                         ob.lay.compact = m.p + 4;
                         if (4 + ob.lay.size > m.n) raise("HDF5: compact data overruns its message");
                     } else if (ob.lay.cls == 1) {
+                        need(18);
                         ob.lay.addr = rd(m.p + 2, 8);
                         ob.lay.size = rd(m.p + 10, 8);
                     } else if (ob.lay.cls == 2) {
+                        need(3);
                         ob.lay.ndim = m.p[2];
                         if (ob.lay.ndim < 1 || ob.lay.ndim > IGM_H5_MAXRANK + 1) raise("HDF5: chunk rank");
+                        need(11 + 4 * (size_t)ob.lay.ndim);
                         ob.lay.addr = rd(m.p + 3, 8);
                         for (int d = 0; d < ob.lay.ndim; ++d) ob.lay.cdims[d] = (uint32_t)rd(m.p + 11 + 4 * d, 4);
                     } else {
@@ -284,21 +295,30 @@ struct igm_h5 {
                     break;
                 }
                 case 0x0B: {
+                    auto need = [&](size_t k) {
+                        if (k > m.n) raise("HDF5: filter pipeline message too short (%zu of %zu bytes)", (size_t)m.n, k);
+                    };
+                    need(2);
                     const int ver = m.p[0], nf = m.p[1];
                     size_t o = ver == 1 ? 8 : 2;
+                    need(o);
                     for (int k = 0; k < nf; ++k) {
                         Filter f;
+                        need(o + 2);
                         f.id = (int)rd(m.p + o, 2);
                         size_t namelen = 0;
                         if (ver == 1 || f.id >= 256) {
+                            need(o + 4);
                             namelen = rd(m.p + o + 2, 2);
                             o += 2;
                         }
+                        need(o + 6);
                         f.flags = (int)rd(m.p + o + 2, 2);
                         const int ncd = (int)rd(m.p + o + 4, 2);
                         o += 6;
                         if (ver == 1) namelen = (namelen + 7) & ~size_t(7);
                         o += namelen;
+                        need(o + 4 * (size_t)ncd);
                         for (int c = 0; c < ncd; ++c) f.cd.push_back((uint32_t)rd(m.p + o + 4 * c, 4));
                         o += 4 * (size_t)ncd;
                         if (ver == 1 && (ncd & 1)) o += 4;
@@ -459,7 +479,13 @@ struct igm_h5 {
             }
             const uint32_t nbytes = (uint32_t)rd(key, 4), mask = (uint32_t)rd(key + 4, 4);
             int64_t off[IGM_H5_MAXRANK];
-            for (int d = 0; d < r; ++d) off[d] = (int64_t)rd(key + 8 + 8 * d, 8);
+            for (int d = 0; d < r; ++d) {
+                off[d] = (int64_t)rd(key + 8 + 8 * d, 8);
+                // a chunk must start inside the dataset (the copy below writes from there)
+                if (off[d] < 0 || off[d] >= ob.s.dims[d] || (ob.lay.cdims[d] && off[d] % ob.lay.cdims[d]))
+                    raise("HDF5: chunk offset %lld outside dimension %d (extent %lld)", (long long)off[d], d,
+                          (long long)ob.s.dims[d]);
+            }
             const uint8_t* src = at(child, nbytes);
             std::vector<uint8_t> data(src, src + nbytes);
             unfilter(data, craw, ob.filters, mask, es);
@@ -655,6 +681,10 @@ extern "C" int igm_h5_info_of(igm_h5* f, const char* path, const char* attr, igm
         info->rank = s.rank;
         for (int d = 0; d < s.rank; ++d) info->dims[d] = s.dims[d];
         info->nelem = s.nelem;
+        // contiguous raw data must lie inside the file (checked here, before a caller
+        // allocates the dataset's size)
+        if (!tg.a && tg.ob.lay.cls == 1 && tg.ob.lay.addr != kUndef && tg.ob.filters.empty())
+            (void)f->at(tg.ob.lay.addr, (uint64_t)s.nelem * (uint64_t)t.size);
         info->layout = tg.a ? -1 : tg.ob.lay.cls;
         info->nfilter = tg.a ? 0 : (int)tg.ob.filters.size();
         info->data_offset = (!tg.a && tg.ob.lay.cls == 1 && tg.ob.lay.addr != kUndef && tg.ob.filters.empty())

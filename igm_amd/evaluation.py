@@ -50,7 +50,6 @@ def haploid_counts(xyz, radii, contact_range, copy_ptr, copy_idx, ctx=None, devi
     """The contact counts with the copies summed on the device (igm_contact_map_haploid):
     (nhap, nhap) int32, entry (a, b) = sum of counts[a_k, b_l] over the copies -- no
     (nbead, nbead) intermediate on the host."""
-    c = ctx or _lib.context(device)
     xyz = np.ascontiguousarray(xyz, np.float32)
     radii = np.ascontiguousarray(radii, np.float32)
     copy_ptr = np.ascontiguousarray(copy_ptr, np.int32)
@@ -59,6 +58,10 @@ def haploid_counts(xyz, radii, contact_range, copy_ptr, copy_idx, ctx=None, devi
         raise ValueError('xyz must be (nbead, nstruct, 3) and radii (nbead,)')
     nbead, S = xyz.shape[0], xyz.shape[1]
     nhap = len(copy_ptr) - 1
+    if nhap < 1 or copy_ptr[0] != 0 or np.any(np.diff(copy_ptr) < 0) or copy_ptr[-1] != len(copy_idx) or \
+            len(copy_idx) != nbead:
+        raise ValueError('copy_ptr must be non-decreasing from 0 to len(copy_idx) == nbead')
+    c = ctx or _lib.context(device)
     out = np.empty((nhap, nhap), np.int32)
     rc = c.lib.igm_contact_map_haploid(c.h, 0, xyz.ctypes.data, nbead, S, radii.ctypes.data, float(contact_range),
                                        copy_ptr.ctypes.data, copy_idx.ctypes.data, nhap, out.ctypes.data)

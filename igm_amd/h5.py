@@ -144,7 +144,10 @@ class File(object):
                        'read %s' % path)
                 out.append(buf.raw[:n.value].decode())
             return out[0] if inf.rank == 0 else np.array(out, dtype=object).reshape(shape)
-        a = np.empty(shape, _numpy_dtype(inf))
+        try:
+            a = np.empty(shape, _numpy_dtype(inf))
+        except MemoryError:
+            raise OSError('read %s: %d elements cannot be allocated (corrupt extent?)' % (path, inf.nelem))
         _check(lib().igm_h5_read(self.h, _b(path), _b(attr), a.ctypes.data if a.size else None, a.nbytes),
                'read %s' % path)
         return a[()] if inf.rank == 0 else a

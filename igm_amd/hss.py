@@ -99,14 +99,25 @@ def update_hss(path, **changes):
     top-level dataset): the reference's HssFile.set_* calls.  The result is
     contiguous, so a chunked (h5py-written) file becomes memory-mappable."""
     with h5.File(path) as f:
-        tree = read_tree(f)
+        # contiguous coordinates stream from a memory map of the old file instead of
+        # being read into memory and copied (the 200 kb pop=1000 population is 360 MB)
+        big = 'coordinates' not in changes and 'coordinates' in f.keys('/') and \
+            f.data_offset('coordinates') is not None
+        tree = read_tree(f, skip=('coordinates',) if big else ())
+        if big:
+            off, shape = f.data_offset('coordinates'), f.shape('coordinates')
+    if big:
+        tree['coordinates'] = np.memmap(path, np.float32, 'r', offset=off, shape=shape)
     for k, v in changes.items():
         if k in ('violation', 'nstruct', 'nbead', 'version'):
             tree['@' + k] = {'violation': np.float64, 'nstruct': np.int64, 'nbead': np.int64,
                              'version': np.int32}[k](v)
         else:
             tree[k] = v
-    h5.write(path, tree)
+    tmp = path + '.update.tmp'  # the old file is still mapped: write beside it, then rename
+    h5.write(tmp, tree)
+    del tree
+    os.replace(tmp, path)
 
 
 def coordinates_memmap(path, mode='r'):

@@ -260,6 +260,9 @@ class AMIteration(object):
         if self.world > 1:
             pairs_u8, np_tot = gather_rows(pairs_u8, self.npairs, pair_dtype.itemsize, self.group)
             pairs_u8 = pairs_u8[:np_tot * pair_dtype.itemsize]
+        # the score is a collective (all_reduce over the ranks): every rank computes it
+        # before the non-writers leave
+        score = self.violation_score() if hasattr(self, 'stats') else np.nan
         self._sync()
         if self.rank != 0:
             return
@@ -272,8 +275,7 @@ class AMIteration(object):
         for h in range(len(cp) - 1):
             copy[ci[cp[h]:cp[h + 1]]] = np.arange(cp[h + 1] - cp[h], dtype=np.int32)
         from . import h5
-        tree = {'@version': np.int32(2), '@violation': np.float64(self.violation_score() if hasattr(self, 'stats')
-                                                                   else np.nan),
+        tree = {'@version': np.int32(2), '@violation': np.float64(score),
                 '@nstruct': np.int64(self.S_total), '@nbead': np.int64(self.nbead),
                 'coordinates': crd, 'radii': self.bead_radii.cpu().numpy(),
                 'index': hss.index_tree(chrom, copy, cp, ci),
@@ -296,7 +298,9 @@ class AMIteration(object):
             pi, pj, plast = f.read('igm_amd/pair_i'), f.read('igm_amd/pair_j'), f.read('igm_amd/plast')
         if len(pi) != self.npairs_total:
             raise ValueError('checkpoint %s holds a different pair list' % path)
-        s0 = int(self.sids[0])
+        # checkpoint() wrote the ranks' blocks in rank order: this rank's structures are
+        # columns rank*S_local .. (whatever its first structure id is)
+        s0 = self.rank * self.S_local
         x = np.zeros((self.S_local, self.natom, 3), np.float32)
         x[:, :self.nbead] = crd[:, s0:s0 + self.S_local].transpose(1, 0, 2)
         x[:, self.nbead:] = extra[s0:s0 + self.S_local]

@@ -23,7 +23,8 @@ scheduler instead of ipyparallel, restartable at batch granularity.
 
 Storage.  The population, the Hi-C input and the A-step rows are the reference's own
 HDF5 files, read and written by the native reader/writer of this package (igm_amd.h5
-over csrc/h5io.cpp; h5py is not importable here): `<structure_output>` ending in
+over csrc/h5io.cpp; no libhdf5 in the product path, the files are checked with h5py in
+tests/test_h5py_pin.py): `<structure_output>` ending in
 .hss is an alabtools HssFile (coordinates (nbead, nstruct, 3) float32 bead-major,
 index, radii, summary), `input_matrix` a .hcs Contactmatrix, `actdist_file` an
 actdist.hdf5 {row, col, dist, prob}.  Files this package writes are contiguous, so

@@ -30,10 +30,18 @@ def main():
         rows = it.rows[:it.nrows * 16].cpu().numpy()
         it.mstep()
         score = it.violation_score()
+        # checkpoint after a step is a collective (the violation score is summed over
+        # the ranks before rank 0 writes); every rank then resumes its own block
+        ck = os.path.join(os.environ['IGM_DIST_OUT'], 'ckpt.hss')
+        it.checkpoint(ck)
+        dist.barrier()
+        back = I.iteration(inp, 'cuda:0', s0, s1, rank, world)
+        back.restore(ck)
+        restored = back.xyz.cpu().numpy()
         np.savez(os.path.join(os.environ['IGM_DIST_OUT'], 'rank%d.npz' % rank), rows=rows,
                  ptr=it.hic_ptr.cpu().numpy(), bonds=it.hic_bonds[:it.nbonds * 16].cpu().numpy(),
                  xyz=it.xyz.cpu().numpy(), stats=it.stats.cpu().numpy(), score=np.float64(score),
-                 info=it.info.cpu().numpy(), s0=s0, s1=s1)
+                 info=it.info.cpu().numpy(), s0=s0, s1=s1, restored=restored)
     finally:
         dist.destroy_process_group()
 

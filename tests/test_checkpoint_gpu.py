@@ -37,3 +37,19 @@ def test_resume_from_checkpoint_is_bitwise_the_uninterrupted_run(tmp_path):
     assert store.nstruct == 4 and np.array_equal(store.copy_ptr, inp['pop']['copy_ptr'])
     h = hss.Hss(path)
     assert np.isfinite(h.violation)
+
+
+@pytest.mark.gpu
+def test_restore_a_shard_whose_first_structure_is_not_zero(tmp_path):
+    """A single-rank shard of structures 4..7 (first_sid 4, as bench.py's ranks pass):
+    the checkpoint holds its 4 structures in columns 0..3, and restore() reads them
+    back from there (not from column first_sid)."""
+    inp = inputs(nstruct=8)
+    path = str(tmp_path / 'ckpt.hss')
+    a = iteration(inp, 'cuda:0', 4, 8)
+    a.step()
+    a.checkpoint(path)
+    b = iteration(inp, 'cuda:0', 4, 8)
+    b.restore(path)
+    assert np.array_equal(b.xyz.cpu().numpy(), a.xyz.cpu().numpy())
+    assert b.step_no == a.step_no

@@ -55,4 +55,5 @@ def test_gpu_two_ranks_equal_one_rank(tmp_path):
         assert p['bonds'].tobytes() == bonds[ptr[s0] * 16:ptr[s1] * 16].tobytes()
         assert np.array_equal(p['ptr'], ptr[s0:s1 + 1] - ptr[s0])
         assert float(p['score']) == score
+        assert np.array_equal(p['restored'], xyz[s0:s1])  # checkpoint after a step, resumed per rank
     assert len(rows) > 1000 and ptr[-1] > 1000

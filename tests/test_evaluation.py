@@ -129,5 +129,18 @@ def test_gpu_haploid_counts_equal_summed_copies(pop):
 @pytest.mark.gpu
 def test_gpu_haploid_counts_rejects_bad_copy_index(pop):
     crd, r = pop['coordinates'][:4, :3], pop['radii'][:4]
-    with pytest.raises(RuntimeError):
+    with pytest.raises((ValueError, RuntimeError)):
         EV.haploid_counts(crd, r, 2.0, np.array([0, 2, 3]), np.array([0, 1, 1]))  # bead 1 twice, 2 and 3 missing
+    with pytest.raises(RuntimeError):  # passes the host checks, the library finds the repeat
+        EV.haploid_counts(crd, r, 2.0, np.array([0, 2, 4]), np.array([0, 1, 1, 3]))
+
+
+def test_haploid_counts_rejects_inconsistent_copy_ptr_on_the_host():
+    """copy_ptr past copy_idx or decreasing is refused before any library call (the
+    C entry point reads copy_idx[k] for k < copy_ptr[nhap])."""
+    crd = np.zeros((4, 2, 3), np.float32)
+    r = np.ones(4, np.float32)
+    for cp, ci in (([0, 2, 9], [0, 1, 2, 3]), ([0, 3, 2, 4], [0, 1, 2, 3]), ([1, 2, 4], [0, 1, 2, 3]),
+                   ([0, 2, 3], [0, 1, 2])):
+        with pytest.raises(ValueError):
+            EV.haploid_counts(crd, r, 2.0, np.array(cp), np.array(ci))

@@ -8,10 +8,10 @@ compared with the arrays tests/golden/make_golden.py extracted from the same fil
 with h5py, and the .hcs read natively feeds select_pairs to reproduce the reference
 setup()'s pair batches.  (Those tests skip where /root/reference is absent.)
 Writer: round trips of every type / shape the IGM files use, the demo .hss rewritten
-member for member, and an independent structural walk (tests/h5_inspect.py).  That
-libhdf5 itself opens the written files is PARITY UNPINNED: no libhdf5/h5py exists in
-this image; the writer emits the structures h5py writes (observed byte for byte in the
-reference files), only contiguous instead of chunked."""
+member for member, and an independent structural walk (tests/h5_inspect.py).  libhdf5
+itself opening the written files (h5py 3.3.0 / libhdf5 1.10.6 under the build image's
+/opt/conda/bin/python3.9) is pinned in tests/test_h5py_pin.py; the datasets are
+contiguous instead of chunked, which h5py reads like the chunked originals."""
 import json
 import os
 
@@ -192,3 +192,54 @@ def test_errors_are_loud(tmp_path):
     with pytest.raises(OSError):
         with h5.File(p) as f:
             f.read('a')
+
+
+FUZZ = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from igm_amd import h5, hss
+src, n, seed = sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+data = open(src, 'rb').read()
+rng = np.random.default_rng(seed)
+ok = bad = 0
+for it in range(n):
+    b = bytearray(data)
+    if it % 3 == 0:
+        b = b[:int(rng.integers(0, len(b)))]
+    else:
+        hi = min(len(b), 1 << 16)  # the metadata (superblock, headers, B-trees) sits in front
+        for _ in range(int(rng.integers(1, 8))):
+            b[int(rng.integers(0, hi))] = int(rng.integers(0, 256))
+    p = src + '.fuzz'
+    open(p, 'wb').write(bytes(b))
+    try:
+        with h5.File(p) as f:
+            hss.read_tree(f)
+        ok += 1
+    except (OSError, ValueError, UnicodeDecodeError):
+        bad += 1
+print(ok, bad)
+'''
+
+
+@pytest.mark.parametrize('which', ['written', 'reference'])
+def test_corrupted_files_fail_cleanly(tmp_path, which):
+    """Truncated files and files with random bytes changed in their metadata either
+    read or raise; the reader never reads past the mapping or writes out of bounds
+    (a crash would kill the child process, so the loop runs in one)."""
+    import subprocess
+    import sys
+    if which == 'reference':
+        if not os.path.exists(HSS_T):
+            pytest.skip('reference demo files absent')
+        src = str(tmp_path / 'ref.hss')
+        open(src, 'wb').write(open(HSS_T, 'rb').read())
+    else:
+        src = str(tmp_path / 'own.h5')
+        h5.write(src, _tree(np.random.default_rng(3)))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, '-c', FUZZ, root, src, '150', '11'], stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:]
+    ok, bad = map(int, r.stdout.split()[-2:])
+    assert ok + bad == 150 and bad > 0
