@@ -52,8 +52,10 @@ def index_tree(chrom, copy, copy_ptr, copy_idx, chrom_sizes=None, start=None, en
                label=None, custom_tracks='{}'):
     n = len(chrom)
     chrom = np.asarray(chrom, np.int32)
-    if chrom_sizes is None:
-        chrom_sizes = np.bincount(chrom[chrom >= 0], minlength=int(chrom.max()) + 1 if n else 0)
+    if chrom_sizes is None:  # alabtools Index.chrom_sizes: beads of every (chromosome, copy) run, in order
+        key = chrom.astype(np.int64) * 64 + np.asarray(copy, np.int64)
+        starts = np.concatenate([[0], np.nonzero(np.diff(key))[0] + 1, [n]]) if n else np.zeros(1, np.int64)
+        chrom_sizes = np.diff(starts)
     return {'chrom': chrom, 'copy': np.asarray(copy, np.int32),
             'start': np.zeros(n, np.int32) if start is None else np.asarray(start, np.int32),
             'end': np.zeros(n, np.int32) if end is None else np.asarray(end, np.int32),
@@ -151,6 +153,8 @@ class Hss(object):
             self.chrom = f.read('index/chrom').astype(np.int32)
             self.copy = f.read('index/copy').astype(np.int32)
             self.copy_ptr, self.copy_idx = copy_index_arrays(f.read('index/copy_index'))
+            self.chrom_sizes = f.read('index/chrom_sizes').astype(np.int64) if 'chrom_sizes' in f.keys('index') \
+                else None
             names = f.keys('/')
             self.summary = f.read('summary') if 'summary' in names else None
 

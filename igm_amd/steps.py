@@ -304,6 +304,7 @@ class PopulationStore(object):
             self.radii, self.chrom, self.copy = h.radii, h.chrom, h.copy
             self.copy_ptr, self.copy_idx = h.copy_ptr, h.copy_idx
             self.hap_chrom = self.chrom[self.copy_idx[self.copy_ptr[:-1]]]
+            self.chrom_sizes = h.chrom_sizes
         else:
             meta = np.load(path + '.index.npz')
             self.radii = meta['radii'].astype(np.float32)
@@ -312,6 +313,11 @@ class PopulationStore(object):
             self.copy_ptr = meta['copy_ptr'].astype(np.int32)
             self.copy_idx = meta['copy_idx'].astype(np.int32)
             self.hap_chrom = meta['hap_chrom'].astype(np.int32) if 'hap_chrom' in meta else self.chrom
+            self.chrom_sizes = meta['chrom_sizes'].astype(np.int64) if 'chrom_sizes' in meta else None
+        if self.chrom_sizes is None:  # index.chrom_sizes: the beads of every (chromosome, copy) run in order
+            key = self.chrom.astype(np.int64) * 64 + self.copy
+            starts = np.concatenate([[0], np.nonzero(np.diff(key))[0] + 1, [len(key)]])
+            self.chrom_sizes = np.diff(starts).astype(np.int64)
         self.nbead = len(self.radii)
 
     @staticmethod
@@ -344,6 +350,12 @@ class PopulationStore(object):
             with open(self.path + '.summary.json', 'w') as f:
                 f.write(text)
 
+    def write_violation(self, violation):
+        """the population's 'violation' attribute (HssFile.set_violation)"""
+        if self.is_hss:
+            from . import hss
+            hss.update_hss(self.path, violation=violation)
+
     def read_summary(self):
         if self.is_hss:
             from . import hss
@@ -372,6 +384,177 @@ def read_input_matrix(path):
     return hss.read_hcs(path)
 
 
+# ------------------------------------------------------------------ config semantics
+_RAISE = object()
+# the defaults of igm/core/defaults/config_schema.json this layer reads (Config.get
+# falls back to them when the key is absent and no explicit default is given,
+# core/config.py:98-115)
+SCHEMA_DEFAULTS = {
+    'model/init_radius': 5000, 'model/restraints/excluded/evfactor': 1.0,
+    'model/restraints/envelope/nucleus_shape': 'sphere', 'model/restraints/envelope/nucleus_radius': 5000.0,
+    'model/restraints/envelope/nucleus_semiaxes': [5000.0, 5000.0, 5000.0],
+    'model/restraints/envelope/volumes_idx': [0], 'model/restraints/envelope/volume_prefix': '',
+    'model/restraints/envelope/nucleus_kspring': 1, 'model/restraints/polymer/contact_range': 2.0,
+    'model/restraints/polymer/polymer_bonds_style': 'simple', 'model/restraints/polymer/polymer_kspring': 1.0,
+    'restraints/Hi-C/contact_range': 2.0, 'restraints/Hi-C/contact_kspring': 1.0,
+    'restraints/DamID/contact_range': 0.05, 'restraints/DamID/contact_kspring': 1.0,
+    'restraints/sprite/kspring': 1.0, 'restraints/sprite/radius_kt': 100.0,
+    'restraints/sprite/assignment_file': 'assignment.h5', 'restraints/sprite/tmp_dir': 'tmp_opt',
+    'restraints/sprite/max_chrom_in_cluster': 6, 'restraints/sprite/batch_size': 150,
+    'restraints/sprite/keep_best': 50, 'restraints/FISH/rtype': 'rRpP', 'restraints/FISH/kspring': 1.0,
+    'restraints/FISH/batch_size': 200, 'restraints/FISH/tmp_dir': 'tmp_opt',
+    'optimization/violation_tolerance': 0.05, 'optimization/keep_intermediate_structures': True,
+    'optimization/clean_restart': False,
+}
+
+
+def rget(cfg, key, default=_RAISE):
+    """igm Config.get: the value, else the explicit default, else the schema default."""
+    v = cget(cfg, key, _RAISE)
+    if v is not _RAISE:
+        return v
+    if default is not _RAISE:
+        return default
+    if key in SCHEMA_DEFAULTS:
+        return SCHEMA_DEFAULTS[key]
+    raise KeyError('%s does not exist' % key)
+
+
+def make_absolute_path(path, basedir='.'):
+    """igm.utils.files.make_absolute_path"""
+    if os.path.isabs(path):
+        return path
+    return os.path.abspath(os.path.join(basedir, path))
+
+
+def _h5_tree(path):
+    from . import h5
+    with h5.File(path) as f:
+        return {k.rstrip('/'): f.read(k) for k in f.keys('/') if not k.endswith('/')}
+
+
+def _write_h5(path, tree):
+    """a small result file (written beside, then renamed into place)"""
+    from . import h5
+    tmp = path + '.tmp'
+    h5.write(tmp, tree)
+    os.replace(tmp, path)
+
+
+def read_damid_rows(path):
+    """damid_actdist.hdf5 {loc i4, dist f4, prob f4} (DamidActivationDistanceStep.py:332-335)"""
+    from ._lib import damid_row_dtype
+    if path.endswith('.npz'):
+        d = np.load(path)
+    else:
+        d = _h5_tree(path)
+    rows = np.zeros(len(d['loc']), damid_row_dtype)
+    for k in ('loc', 'dist', 'prob'):
+        rows[k] = d[k]
+    return rows
+
+
+def sprite_assignment_path(cfg):
+    """where SpriteAssignmentStep.reduce writes and ModelingStep.task reads the SPRITE
+    assignment (SpriteAssignmentStep.py:53-56,183-186; ModelingStep.py:459-466)"""
+    tmp = make_absolute_path(rget(cfg, 'restraints/sprite/tmp_dir', 'sprite'),
+                             cget(cfg, 'parameters/tmp_dir', 'tmp'))
+    return make_absolute_path(rget(cfg, 'restraints/sprite/assignment_file', 'assignment.h5'), tmp)
+
+
+def fish_assignment_path(cfg):
+    """the FISH assignment ModelingStep.task reads: the file the last FishAssignmentStep
+    recorded in runtime/FISH/fish_assignment_file; without one, ModelingStep's own
+    formula (ModelingStep.py:485-492 -- the reference's A-step writes under
+    restraints/FISH/fish_dir instead, FishAssignmentStep.py:376-387, so a config relies
+    on the runtime entry)"""
+    rt = cget(cfg, 'runtime/FISH/fish_assignment_file', None)
+    if rt:
+        return rt
+    tmp = make_absolute_path(rget(cfg, 'restraints/FISH/tmp_dir', 'FISH'), cget(cfg, 'parameters/tmp_dir', 'tmp'))
+    return make_absolute_path(rget(cfg, 'restraints/FISH/fish_file', 'fish_assignment.h5'), tmp)
+
+
+_VOLUMES = {}
+
+
+def _volume(path):
+    from . import volume as V
+    key = (path, os.path.getmtime(path))
+    if key not in _VOLUMES:
+        _VOLUMES.clear()
+        _VOLUMES[key] = V.read_volume(path)
+    return _VOLUMES[key]
+
+
+def envelope_section(cfg, sids):
+    """model/restraints/envelope as an assemble envelope spec (ModelingStep.py:252-277)"""
+    from . import assemble as A
+    shape = rget(cfg, 'model/restraints/envelope/nucleus_shape')
+    k = rget(cfg, 'model/restraints/envelope/nucleus_kspring')
+    if shape == 'sphere':
+        return A.envelope_spec('sphere', radius=rget(cfg, 'model/restraints/envelope/nucleus_radius'), k=k)
+    if shape == 'ellipsoid':
+        return A.envelope_spec('ellipsoid', semiaxes=rget(cfg, 'model/restraints/envelope/nucleus_semiaxes'), k=k)
+    if shape == 'exp_map':
+        prefix = rget(cfg, 'model/restraints/envelope/volume_prefix')
+        idx = rget(cfg, 'model/restraints/envelope/volumes_idx')
+        files = [prefix + str(idx[int(s) % len(idx)]) + '.bin' for s in sids]  # ModelingStep.py:265-270
+        uniq = sorted(set(files))
+        return {'shape': 'exp_map', 'k': float(k), 'repr_k': k, 'files': uniq,
+                'volumes': [_volume(f) for f in uniq], 'struct_map': np.array([uniq.index(f) for f in files], np.int32)}
+    raise NotImplementedError('Envelope (%s) not implemented' % shape)
+
+
+def modeling_spec(cfg, sids):
+    """Everything ModelingStep.task adds to a structure (ModelingStep.py:213-503) for the
+    structures `sids`, as an igm_amd.assemble spec.  Sections this layer does not
+    implement raise NotImplementedError -- none is dropped silently."""
+    rs = cget(cfg, 'model/restraints', {}) or {}
+    R = cfg.get('restraints', {}) or {}
+    for key in ('tracing', 'nuclDamID'):
+        if key in R:
+            raise NotImplementedError('restraints/%s is not implemented on the hip kernel' % key)
+    if 'nucleolus' in rs:
+        # ModelingStep.py:306-327: GenEnvelope of a second map; the reference logs an
+        # undefined name unless the envelope is exp_map (D8), and one structure would need
+        # two maps -- not supported by igm_mstep_set_volumes
+        raise NotImplementedError('model/restraints/nucleolus is not implemented on the hip kernel')
+    spec = {'evfactor': float(rget(cfg, 'model/restraints/excluded/evfactor')),
+            'protocol': cfg['optimization']['optimizer_options']}
+    if 'polymer' in rs:
+        if rget(cfg, 'model/restraints/polymer/polymer_bonds_style') != 'none':
+            spec['polymer'] = {'contact_range': float(rs['polymer'].get('contact_range', 2.0)),
+                               'kspring': float(rs['polymer'].get('polymer_kspring', 1.0)),
+                               'monitored': rs['polymer'].get('violations', 'true') == 'true',  # D2
+                               'contact_probabilities': cget(cfg, 'runtime/consecutive_contact_probabilities')}
+    else:  # PolymerDistrib on the PolymerAssignmentStep targets (ModelingStep.py:236-249)
+        pr = R['polymer']
+        d = _h5_tree(cget(cfg, 'runtime/polymer/assignment_file'))
+        spec['polymer'] = {'distrib': (d['loci'], d['nn_dist']), 'tolerance': float(pr['tolerance']),
+                           'kspring': float(pr['polymer_kspring']),
+                           'monitored': pr.get('violations', 'true') == 'true'}
+    spec['envelope'] = envelope_section(cfg, sids)
+    if 'Hi-C' in R:
+        act = cget(cfg, 'runtime/Hi-C/actdist_file', None)
+        spec['hic'] = {'rows': read_rows(act) if act else np.zeros(0, row_dtype),
+                       'contact_range': float(rget(cfg, 'restraints/Hi-C/contact_range', 2.0)),
+                       'k': float(rget(cfg, 'restraints/Hi-C/contact_kspring', 0.05))}
+    if 'DamID' in R:
+        spec['damid'] = {'rows': read_damid_rows(cget(cfg, 'runtime/DamID/damid_actdist_file')),
+                         'contact_range': float(rget(cfg, 'restraints/DamID/contact_range', 2.0)),
+                         'k': float(rget(cfg, 'restraints/DamID/contact_kspring', 0.05))}
+    if 'sprite' in R:
+        a = _h5_tree(sprite_assignment_path(cfg))
+        spec['sprite'] = {'assignment': a['assignment'], 'indptr': a['indptr'], 'selected': a['selected'],
+                          'volume_fraction': float(cfg['runtime']['sprite']['volume_fraction']),
+                          'k': float(R['sprite']['kspring'])}
+    if 'FISH' in R:
+        spec['fish'] = {'data': _h5_tree(fish_assignment_path(cfg)), 'rtype': R['FISH']['rtype'],
+                        'tol': float(cfg['runtime']['FISH']['tol']), 'k': float(R['FISH']['kspring'])}
+    return spec
+
+
 # ------------------------------------------------------------------ kernels
 def _hip_actdist(store, pairs, cfg, device):
     from . import astep, _lib
@@ -381,33 +564,35 @@ def _hip_actdist(store, pairs, cfg, device):
                                  int(cget(cfg, 'runtime/Hi-C/iter_corr_knob', 1)), ctx=_lib.context(device))
 
 
-def _hip_mstep(store, sids, rows, cfg, device):
-    """ModelingStep.task for a batch of structures on one GPU: Hi-C selection, the
-    annealing protocol + CG, violation records.  Returns dict(xyz (S, nbead, 3) f32,
-    info (S) optinfo, stats (S, ncls, 104))."""
-    from . import mstep, _lib
-    ctx = _lib.context(device)
-    prm, atoms, poly, chrom, cr, k, env_scale = modeling_inputs(store, cfg)
+def batch_coordinates(store, sids):
+    """(S, nbead, 3) float32 struct-major coordinates of the structures sids"""
     crd = store.coordinates()
-    x = np.zeros((len(sids), atoms.n, 3), np.float32)
-    x[:, :atoms.nbead] = np.asarray(crd[:, sids, :]).transpose(1, 0, 2)
-    ptr, bonds, bcls = mstep.hic_select(x, atoms.radii, chrom, rows['row'], rows['col'], rows['dist'], cr, k,
-                                        ctx=ctx)
+    return np.ascontiguousarray(np.asarray(crd[:, sids, :]).transpose(1, 0, 2), np.float32)
+
+
+def _hip_mstep(store, sids, cfg, device):
+    """ModelingStep.task for a batch of structures on one GPU: the restraints of
+    modeling_spec assembled on the device (Hi-C and DamID selections), the annealing
+    protocol + CG, violation records.  Returns dict(xyz (S, nbead, 3) f32, info (S)
+    optinfo, stats (S, ncls, 104), names [per structure: vstat key per class])."""
+    from . import _lib, assemble as A
+    ctx = _lib.context(device)
+    spec = modeling_spec(cfg, sids)
+    b = A.build(batch_coordinates(store, sids), sids, store, spec, ctx)
     seeds = M.lammps_seeds(cget(cfg, 'optimization/optimizer_options/seed', 6535), sids,
                            cget(cfg, 'runtime/step_no', 1))
-    xo, info = mstep.run(prm, x, atoms.radii, atoms.flags, poly, ptr, bonds, seeds, ctx=ctx)
-    stats = mstep.violations(prm, xo, atoms.radii, atoms.flags, poly, np.full(len(poly), M.CLASS_POLYMER, np.int32),
-                             ptr, bonds, bcls, [cr, cr, cr], env_scale,
-                             float(cget(cfg, 'optimization/violation_tolerance', 0.05)), ctx=ctx)
-    return {'xyz': xo[:, :atoms.nbead], 'info': info, 'stats': stats}
+    xo, info, stats = A.run(b, seeds, float(rget(cfg, 'optimization/violation_tolerance')), ctx)
+    return {'xyz': xo[:, :b.nbead], 'info': info, 'stats': stats,
+            'names': [b.vstat_names(q) for q in range(len(sids))]}
 
 
 KERNELS = {'hip': {'actdist': _hip_actdist, 'mstep': _hip_mstep}}
 
 
 def modeling_inputs(store, cfg):
-    """The per-batch model of ModelingStep.task (Hi-C configuration): steric + polymer +
-    sphere/ellipsoid envelope, params of optimization/optimizer_options."""
+    """The Hi-C configuration's shared model pieces (steric + polymer + nucleus envelope,
+    params of optimization/optimizer_options): prm, atoms, poly, chrom, Hi-C contact
+    range and k, envelope violation scale."""
     rs = cget(cfg, 'model/restraints', {})
     env = rs.get('envelope', {'nucleus_shape': 'sphere', 'nucleus_radius': 5500.0, 'nucleus_kspring': 1.0})
     if env['nucleus_shape'] == 'sphere':
@@ -516,11 +701,10 @@ class ModelingStep(Step):
 
     def task(self, batch, device):
         store = PopulationStore(self.cfg['optimization']['structure_output'])
-        act = cget(self.cfg, 'runtime/Hi-C/actdist_file', None)
-        rows = read_rows(act) if act else np.zeros(0, row_dtype)
-        res = _kernel(self.cfg, 'mstep')(store, np.asarray(batch['sids']), rows, self.cfg, device)
+        res = _kernel(self.cfg, 'mstep')(store, np.asarray(batch['sids']), self.cfg, device)
         tmp = batch['out'] + '.part.npz'
-        np.savez(tmp, xyz=res['xyz'], info=res['info'].view(np.uint8), stats=res['stats'])
+        np.savez(tmp, xyz=res['xyz'], info=res['info'].view(np.uint8), stats=res['stats'],
+                 names=json.dumps(res['names']))
         os.replace(tmp, batch['out'])
 
     def reduce(self):
@@ -528,28 +712,31 @@ class ModelingStep(Step):
         (ModelingStep.py:612-746): coordinates into the population, the summary JSON,
         runtime/violation_score."""
         from ._lib import optinfo_dtype
-        from .summary import PopulationSummary, vstat_from_record, restraint_key
+        from .summary import PopulationSummary, vstat_from_record
         store = PopulationStore(self.cfg['optimization']['structure_output'])
         crd = store.coordinates('r+')
         summ = PopulationSummary(crd.shape[1])
-        env = cget(self.cfg, 'model/restraints/envelope', {'nucleus_shape': 'sphere', 'nucleus_radius': 5500.0,
-                                                           'nucleus_kspring': 1.0})
-        # vstat keys: repr() of the reference restraints, the config's numbers as written
-        abc = [env.get('nucleus_radius')] * 3 if env['nucleus_shape'] == 'sphere' else env['nucleus_semiaxes']
-        names = ['Polymer', 'interHiC', 'intraHiC',
-                 restraint_key('Envelope', shape=env['nucleus_shape'], k=env.get('nucleus_kspring', 1.0),
-                               a=abc[0], b=abc[1], c=abc[2])]
         for b in self.argument_list:
             res = np.load(b['out'])
             info = res['info'].view(optinfo_dtype)
+            names = json.loads(str(res['names']))  # vstat key per class (repr() of the restraints)
             for q, sid in enumerate(b['sids']):
                 crd[:, sid, :] = res['xyz'][q]
                 opt = {'final-energy': float(info['final_energy'][q]), 'pair-energy': float(info['pair_energy'][q]),
                        'bond-energy': float(info['bond_energy'][q]),
                        'thermo': {'Temp': float(info['temp'][q])}}
-                summ.set_structure(sid, vstat_from_record(res['stats'][q], names), opt)
+                summ.set_structure(sid, vstat_from_record(res['stats'][q], names[q]), opt)
         crd.flush()
         del crd
         score = float(summ.violation_score())
         store.write_summary(summ.to_json(), score)
         cset(self.cfg, 'runtime/violation_score', score)
+
+
+# ------------------------------------------------------------------ the other steps
+from .assign_steps import (DamidActivationDistanceStep, FishAssignmentStep, PolymerAssignmentStep,  # noqa: E402
+                           SpriteAssignmentStep, KERNELS_HIP as _A_HIP)
+from .init_steps import RandomInit, RelaxInit, KERNELS_HIP as _I_HIP  # noqa: E402
+
+KERNELS['hip'].update(_A_HIP)
+KERNELS['hip'].update(_I_HIP)

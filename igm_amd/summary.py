@@ -38,6 +38,8 @@ def vstat_from_record(rec, names):
     edges = _edges().tolist()
     out = {}
     for c, name in enumerate(names):
+        if name is None:  # a record class the configuration does not monitor
+            continue
         out[name] = {'histogram': {'edges': edges, 'counts': [int(x) for x in rec[c, :101]]},
                      'violated_restr': int(rec[c, 101]), 'n_violations': int(rec[c, 102]),
                      'n_imposed': int(rec[c, 103])}

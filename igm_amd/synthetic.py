@@ -115,12 +115,18 @@ def occupancy_radii(start, end, occupancy=0.4, nucleus_radius=5500.0):
     return ((rho * bp) / (4.0 / 3.0 * np.pi)) ** (1.0 / 3.0)
 
 
-def population_200kb(nstruct, first_sid=0, init_radius=7000.0):
+def population_200kb(nstruct, first_sid=0, init_radius=7000.0, semiaxes=None):
     """Config C: 200 kb hg38 male diploid, synthetic territories (same recipe as
-    population_2mb).  Same keys as population_2mb."""
+    population_2mb).  Same keys as population_2mb.  With `semiaxes` (config D's
+    ellipsoid) the radii follow the occupancy of the ellipsoid's volume
+    (_preprocess.py:153-162 with the volume-equivalent radius: 118.5 nm for
+    ELLIPSOID_D) and the territories are stretched by semiaxes / 5500."""
     ix = male_diploid_index(200000)
-    radii = occupancy_radii(ix['start'], ix['end']).astype(np.float32)
+    req = 5500.0 if semiaxes is None else float(np.prod(semiaxes)) ** (1.0 / 3.0)
+    radii = occupancy_radii(ix['start'], ix['end'], nucleus_radius=req).astype(np.float32)
     xyz = np.stack([territories(ix['chrom_sizes'], init_radius, 1000 + first_sid + s) for s in range(nstruct)])
+    if semiaxes is not None:
+        xyz = (xyz * (np.asarray(semiaxes, np.float64) / 5500.0)).astype(np.float32)
     return {'xyz': xyz, 'radii': radii, 'chrom': ix['chrom'], 'copy': ix['copy'], 'copy_ptr': ix['copy_ptr'],
             'copy_idx': ix['copy_idx'], 'chrom_sizes': ix['chrom_sizes'], 'hap_chrom': ix['hap_chrom']}
 

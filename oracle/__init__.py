@@ -66,6 +66,8 @@ def _mlib():
         vp, i32, i64, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
         L.oracle_mstep_run.restype = ctypes.c_int
         L.oracle_mstep_run.argtypes = [vp, i32, i32, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, i32]
+        L.oracle_mstep_run_sf.restype = ctypes.c_int
+        L.oracle_mstep_run_sf.argtypes = [vp, i32, i32, vp, vp, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32]
         L.oracle_mstep_forces.restype = ctypes.c_int
         L.oracle_mstep_forces.argtypes = [vp, i32, i32, vp, vp, vp, vp, i64, vp, vp, f64, f64, vp, vp]
         L.oracle_mstep_md.restype = ctypes.c_int
@@ -89,7 +91,8 @@ def _bonds(shared, sptr, sbonds, nstruct):
 
 def mstep_run(params, xyz, radii, flags, shared, sptr, sbonds, seeds, nthreads=1):
     """Full protocol (anneal + CG) per structure in fp64.  xyz (S, N, 3) f32 is
-    updated in place (rounded to f32); returns (info, x64)."""
+    updated in place (rounded to f32); returns (info, x64).  flags (N,) shared or
+    (S, N) one row per structure."""
     import ctypes as C
     from igm_amd._lib import optinfo_dtype
     xyz = np.ascontiguousarray(xyz, np.float32)
@@ -100,9 +103,11 @@ def mstep_run(params, xyz, radii, flags, shared, sptr, sbonds, seeds, nthreads=1
     radii = _c(radii, np.float32)
     flags = _c(flags, np.uint32)
     seeds = _c(seeds, np.int32)
-    _mlib().oracle_mstep_run(C.byref(params), S, N, xyz.ctypes.data, radii.ctypes.data, flags.ctypes.data,
-                             shared.ctypes.data, len(shared), sptr.ctypes.data, sbonds.ctypes.data,
-                             seeds.ctypes.data, info.ctypes.data, x64.ctypes.data, int(nthreads))
+    assert flags.shape[-1] == N and (flags.ndim == 1 or flags.shape[0] == S)
+    _mlib().oracle_mstep_run_sf(C.byref(params), S, N, xyz.ctypes.data, radii.ctypes.data, flags.ctypes.data,
+                                N if flags.ndim == 2 else 0, shared.ctypes.data, len(shared), sptr.ctypes.data,
+                                sbonds.ctypes.data, seeds.ctypes.data, info.ctypes.data, x64.ctypes.data,
+                                int(nthreads))
     return xyz, info, x64
 
 

@@ -707,17 +707,27 @@ static void run_one(const igm_mstep_params* p, int natom, float* xyz, const floa
     model_free(&m);
 }
 
+/* fl_stride: 0 = one flag row shared by every structure, natom = a row per structure
+ * (the GPU's IGM_MSTEP_STRUCT_FLAGS: DamID envelope members, SPRITE centroid slots) */
+int oracle_mstep_run_sf(const igm_mstep_params* p, int32_t nstruct, int32_t natom, float* xyz, const float* radii,
+                        const uint32_t* fl, int64_t fl_stride, const igm_bond* shared, int64_t nshared,
+                        const int64_t* sptr, const igm_bond* sbonds, const int32_t* seeds, igm_opt_info* info,
+                        double* xout, int32_t nthreads) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int s = 0; s < nstruct; ++s) {
+        const int64_t b0 = sptr ? sptr[s] : 0, b1 = sptr ? sptr[s + 1] : 0;
+        run_one(p, natom, xyz + (size_t)s * natom * 3, radii, fl + (size_t)s * fl_stride, shared, nshared,
+                sbonds + b0, b1 - b0, seeds[s], &info[s], xout ? xout + (size_t)s * natom * 3 : NULL);
+    }
+    return 0;
+}
+
 int oracle_mstep_run(const igm_mstep_params* p, int32_t nstruct, int32_t natom, float* xyz, const float* radii,
                      const uint32_t* fl, const igm_bond* shared, int64_t nshared, const int64_t* sptr,
                      const igm_bond* sbonds, const int32_t* seeds, igm_opt_info* info, double* xout,
                      int32_t nthreads) {
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
-    for (int s = 0; s < nstruct; ++s) {
-        const int64_t b0 = sptr ? sptr[s] : 0, b1 = sptr ? sptr[s + 1] : 0;
-        run_one(p, natom, xyz + (size_t)s * natom * 3, radii, fl, shared, nshared, sbonds + b0, b1 - b0, seeds[s],
-                &info[s], xout ? xout + (size_t)s * natom * 3 : NULL);
-    }
-    return 0;
+    return oracle_mstep_run_sf(p, nstruct, natom, xyz, radii, fl, 0, shared, nshared, sptr, sbonds, seeds, info, xout,
+                               nthreads);
 }
 
 /* forces (f64) and energies {total, pair, bond, env0..3} */

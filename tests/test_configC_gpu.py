@@ -82,12 +82,18 @@ def _model200(n, nlocal=15000, nlong=1500, seed=31):
 
 
 def test_gpu_200kb_protocol_matches_oracle_and_reruns_bitwise():
+    """16 structures of the metric's 200 kb model with frustrated Hi-C-like restraints,
+    the whole demo protocol shape at x0.02 (940 MD steps + CG), the engines' DEFAULT
+    Verlet skins (GPU 0.7 maxrad, oracle LAMMPS maxrad): the KS statistic of
+    tests/mstep_stats.py (it rejects a 2x bond K or a 2x evfactor) does not separate
+    the GPU population from the fp64 oracle's on E_pair, E_bond, E_env, E_total per
+    bead, the violation fraction and the final Temp; the rerun is bitwise identical.
+    (Rebuild counts differ by construction of the skins and are not compared.)"""
     from igm_amd import mstep
-    n = 8
+    n = 16
     atoms, poly, ptr, sb, x = _model200(n)
     proto = MS.scaled_protocol(syn.DEMO_PROTOCOL, 0.02)  # 4 stages + relax + CG, 940 MD steps
     prm = M.params_from_cfg({'optimization': {'optimizer_options': proto}}, [((5500.0,) * 3, 1.0)])
-    prm.skin = 0.55 * float(atoms.radii.max())  # the same Verlet skin on both sides
     seeds = M.lammps_seeds(6535, np.arange(500, 500 + n), 3)
     xg, ig = mstep.run(prm, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
     xg2, ig2 = mstep.run(prm, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
@@ -96,10 +102,7 @@ def test_gpu_200kb_protocol_matches_oracle_and_reruns_bitwise():
     xo, io, _ = oracle.mstep_run(prm, x.copy(), atoms.radii, atoms.flags, poly, ptr, sb, seeds, nthreads=16)
     sg = MS.population_stats(ig, xg, poly, ptr, sb, atoms.nbead)
     so = MS.population_stats(io, xo, poly, ptr, sb, atoms.nbead)
-    # 8 chaotic trajectories per side: the medians of the per-structure energies per bead
-    # and violation fractions agree within 20 % (the 2x K / 2x evf perturbations of
-    # tests/test_mstep_stats.py move them by 25-140 %)
-    for k in ('pair', 'bond', 'total', 'viol_frac'):
-        a, b = np.median(sg[k]), np.median(so[k])
-        assert abs(a - b) <= 0.2 * max(abs(a), abs(b)) + 1e-9, (k, a, b)
+    sg['env'], so['env'] = ig['env_energy'][:, 0] / atoms.nbead, io['env_energy'][:, 0] / atoms.nbead
+    ok, pv = MS.same_population(sg, so, keys=('pair', 'bond', 'env', 'total', 'viol_frac', 'temp'))
+    assert ok, pv
     assert np.all(ig['temp'] < 1.0) and np.all(io['temp'] < 1.0)

@@ -146,23 +146,28 @@ def test_gpu_cg_matches_oracle(demo, ms):
 
 
 def test_gpu_full_protocol_short(demo, ms):
-    """Whole protocol (4 stages, relax, velocity create, CG) on a shortened schedule:
-    runs, is deterministic, and lands in the oracle's energy range."""
-    pop, g3 = demo
-    sids = list(range(6))
-    atoms, poly, prm, ptr, sb = _bonds_for(demo, sids)
+    """Whole protocol (4 stages, relax, velocity create, CG) on a shortened schedule
+    (300 MD steps per stage): runs, is bitwise deterministic, and -- 16 structures of
+    the demo model with frustrated restraints -- is not separated from the fp64
+    oracle's population by the KS statistic of tests/mstep_stats.py (energies per
+    bead, envelope energy, violation fraction, final Temp, rebuilds at the same skin)."""
+    import mstep_stats as MS
+    from test_mstep_stats import _inputs
+    sids = list(range(16))
+    atoms, poly, ptr, sb, x = _inputs(sids, 1000, 1000)
     p = M.params_from_cfg({'optimization': {'optimizer_options': short_protocol()}}, [((5500.0,) * 3, 1.0)])
-    x = F.struct_major(pop, sids, atoms.n)
+    p.skin = 280.7308  # LAMMPS 'neighbor maxrad bin' on both sides, so rebuild counts compare
     seeds = M.lammps_seeds(6535, sids, 11)
     xg, ig = ms.run(p, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
     xg2, ig2 = ms.run(p, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
     assert np.array_equal(xg, xg2)  # bitwise reproducible
     assert np.all(np.isfinite(xg))
-    xo, io, _ = oracle.mstep_run(p, x.copy(), atoms.radii, atoms.flags, poly, ptr, sb, seeds, nthreads=6)
-    eg = ig['final_energy'] / 3008
-    eo = io['final_energy'] / 3008
-    assert np.all(eg < 50.0) and np.all(eo < 50.0)
-    assert abs(np.median(eg) - np.median(eo)) < 5.0
+    xo, io, _ = oracle.mstep_run(p, x.copy(), atoms.radii, atoms.flags, poly, ptr, sb, seeds, nthreads=16)
+    sg = MS.population_stats(ig, xg, poly, ptr, sb, atoms.nbead)
+    so = MS.population_stats(io, xo, poly, ptr, sb, atoms.nbead)
+    sg['env'], so['env'] = ig['env_energy'][:, 0] / atoms.nbead, io['env_energy'][:, 0] / atoms.nbead
+    ok, pv = MS.same_population(sg, so, keys=('pair', 'bond', 'env', 'total', 'viol_frac', 'temp', 'rebuilds'))
+    assert ok, pv
     assert np.all(ig['temp'] < 0.2)
 
 

@@ -19,45 +19,15 @@ import mstep_stats as MS
 from conftest import GOLDEN
 from igm_amd import steps as ST
 from igm_amd import model as M
-from igm_amd._lib import optinfo_dtype
 
-CALLS = []
-FAIL_AT = {'batch': None}
+import cpu_kernels as CK  # registers optimization/kernel 'cpu_oracle_test'
+
+CALLS = CK.CALLS
+FAIL_AT = CK.FAIL_AT
 
 
 def _oracle_actdist(store, pairs, cfg, device):
-    xyz = np.ascontiguousarray(store.coordinates())
-    rows, _ = oracle.actdist(xyz, store.radii, store.copy_ptr, store.copy_idx, store.hap_chrom, pairs, 2.0,
-                             int(ST.cget(cfg, 'runtime/Hi-C/iter_corr_knob', 1)), nthreads=4)
-    return rows
-
-
-def _oracle_mstep(store, sids, rows, cfg, device):
-    if FAIL_AT['batch'] is not None and int(sids[0]) == FAIL_AT['batch']:
-        raise RuntimeError('injected failure (the GPU box died)')
-    CALLS.append(int(sids[0]))
-    prm, atoms, poly, chrom, cr, k, _ = ST.modeling_inputs(store, cfg)
-    crd = store.coordinates()
-    x = np.zeros((len(sids), atoms.n, 3), np.float32)
-    x[:, :atoms.nbead] = np.asarray(crd[:, sids, :]).transpose(1, 0, 2)
-    sel = oracle.hic_select(x, chrom, rows['row'], rows['col'], rows['dist'])
-    per = []
-    for q in range(len(sids)):
-        keep = sel[q] > 0
-        b = np.zeros(int(keep.sum()), poly.dtype)
-        b['i'], b['j'] = rows['row'][keep], rows['col'][keep]
-        b['r0'] = M.r0_contact(cr, atoms.radii[b['i']], atoms.radii[b['j']]).astype(np.float32)
-        b['k'] = k
-        per.append(b)
-    ptr, sb = M.concat_bonds(per)
-    seeds = M.lammps_seeds(6535, sids, ST.cget(cfg, 'runtime/step_no', 1))
-    xo, info, _ = oracle.mstep_run(prm, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds, nthreads=4)
-    stats = np.zeros((len(sids), 4, 104), np.int64)
-    stats[:, 1, 103] = np.diff(ptr)  # n_imposed of the Hi-C class (enough for the score plumbing)
-    return {'xyz': xo[:, :atoms.nbead], 'info': info, 'stats': stats}
-
-
-ST.KERNELS['cpu_oracle_test'] = {'actdist': _oracle_actdist, 'mstep': _oracle_mstep}
+    return CK.actdist(store, pairs, cfg, device)
 
 
 def _setup(tmp, S=9, fmt='hdf5'):
