@@ -13,6 +13,15 @@ rank owns its own block of 1000 structure ids), Hi-C pairs of the demo .hcs at
 sigma = 0.02, the demo annealing protocol (47 000 MD steps + CG), synthetic
 territory initial coordinates (RandomInit semantics, seeded).
 
+config_C block (the metric's own workload, BASELINE configs[2]): 200 kb diploid,
+pop = --c-total structures STRONG-split over the ranks (default 1000 with several
+GPUs: at 8 GPUs the 125-structure shards of pop=1000, the north-star run; 125 on one
+GPU), Hi-C sigma 0.01, full protocol, the A-step over the whole population after one
+RCCL all-gather; c_warmup + c_steps A/M iterations between barriers, max over ranks.
+CPU baselines (rank 0, N=1): the fp64 C port on the state of the first TIMED step
+(snapshot after the warmup: same coordinates, restraints, seeds), threads = the
+box's CPU share (affinity), at most --cpu-threads.
+
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
 torch.distributed.run (one process per GPU, RCCL).
 """
@@ -40,13 +49,16 @@ def parse():
     ap.add_argument('--nstruct', type=int, default=None, help='structures per GPU (B: 1000, C: 125)')
     ap.add_argument('--sigma', type=float, default=None, help='Hi-C sigma (B: 0.02, C: 0.01)')
     ap.add_argument('--cpu-sample', type=int, default=16, help='structures in the CPU baseline sample (0: skip)')
-    ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--cpu-threads', type=int, default=16, help='at most this many host threads (the box\'s share)')
     ap.add_argument('--no-de', action='store_true', help='skip the configuration D/E A-step measurement')
     ap.add_argument('--sprite-clusters', type=int, default=20000, help='SPRITE clusters in the D/E measurement')
     ap.add_argument('--protocol-scale', type=float, default=1.0,
                     help='scale the MD step counts (only for smoke tests; the metric needs 1.0)')
     ap.add_argument('--no-c', action='store_true', help='skip the config C (200 kb) block of the N=1 line')
     ap.add_argument('--c-steps', type=int, default=1, help='timed A/M iterations of the config C block')
+    ap.add_argument('--c-total', type=int, default=None,
+                    help='config C population split over the ranks (default: 1000 with several GPUs -- the '
+                         'metric -- and the 125-structure shard of pop=1000 at 8 GPUs on one)')
     ap.add_argument('--c-warmup', type=int, default=1, help='warmup A/M iterations of the config C block')
     ap.add_argument('--c-cpu-scale', type=float, default=0.02,
                     help='protocol scale of the config C CPU-baseline sample (0: skip it)')
@@ -55,6 +67,8 @@ def parse():
         a.nstruct = 1000 if a.config == 'B' else 125
     if a.sigma is None:
         a.sigma = 0.02 if a.config == 'B' else 0.01
+    if a.c_total is None:
+        a.c_total = 1000 if int(os.environ.get('WORLD_SIZE', '1')) > 1 else 125
     return a
 
 
@@ -82,48 +96,74 @@ def build_inputs(args, rank):
     return dict(pop=pop, atoms=atoms, xyz=xyz, chrom=chrom, poly=poly, prm=prm, pairs=pairs, first=first)
 
 
-def cpu_baseline(args, it, inp):
-    """The fp64 C restatement of the LAMMPS protocol (oracle/mstep_ref.c, kind
-    'port'), one structure per thread, on a bounded sample of the same workload:
-    the first `cpu_sample` structures of rank 0 from the same initial coordinates
-    and the same Hi-C restraints the GPU M-step of step 0 used."""
+def host_threads(args):
+    """threads for the CPU baselines: --cpu-threads, at most the CPUs this process may
+    run on (on the GPU box os.cpu_count() shows the whole machine, the box's share is
+    the affinity mask)"""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(args.cpu_threads, avail)), avail
+
+
+def step_restraints(it, snap):
+    """The Hi-C restraints the M-step of the step starting from `snap` uses: the A-step
+    and the selection of that step, recomputed on the GPU from the snapshot (the state
+    after the warmup = the first timed step's input)."""
+    import torch
+    it.load_snapshot(snap)
+    it.astep()
+    it.select()
+    torch.cuda.synchronize(it.dev)
+    return it.hic_ptr.cpu().numpy(), it.hic_bonds.cpu().numpy(), snap['xyz'].cpu().numpy(), snap['step_no']
+
+
+def cpu_baseline(args, it, inp, snap):
+    """The fp64 C restatement of the LAMMPS protocol (oracle/mstep_ref.c, kind 'port'),
+    one structure per thread, on a bounded sample of the SAME work as the first timed
+    GPU step: the first `cpu_sample` structures of rank 0 at the state after the
+    warmup, with the Hi-C restraints and LAMMPS seeds of that step."""
     import oracle
     from igm_amd import model as M
     from igm_amd._lib import bond_dtype
+    nth, avail = host_threads(args)
+    ptr, bonds, xall, step_no = step_restraints(it, snap)
+    bonds = bonds.view(bond_dtype)
     n = min(args.cpu_sample, it.S_local)
-    ptr = it.hic_ptr.cpu().numpy()
-    bonds = it.hic_bonds.cpu().numpy().view(bond_dtype)
     sptr = ptr[:n + 1].copy()
     sb = bonds[:sptr[-1]].copy()
-    x = inp['xyz'][:n].copy()
-    seeds = M.lammps_seeds(it.seed, np.arange(n), 0)
+    x = np.ascontiguousarray(xall[:n])
+    seeds = M.lammps_seeds(it.seed, it.sids[:n], step_no)
     t0 = time.perf_counter()
     oracle.mstep_run(inp['prm'], x, inp['atoms'].radii, inp['atoms'].flags, inp['poly'], sptr, sb, seeds,
-                     nthreads=min(args.cpu_threads, n))
+                     nthreads=min(nth, n))
     dt = time.perf_counter() - t0
-    return {'value': n / dt, 'unit': 'structures/s', 'cores': min(args.cpu_threads, n), 'kind': 'port',
-            'sample': '%d structures of config B (full demo protocol, same initial coordinates and Hi-C '
-                      'restraints as GPU step 0), fp64 C restatement, one structure per thread, %.1f s'
-                      % (n, dt)}
+    return {'value': n / dt, 'unit': 'structures/s', 'cores': min(nth, n), 'host_cpus_visible': avail,
+            'kind': 'port',
+            'sample': '%d structures of config B at the state of the first timed step (after %d warmup A/M '
+                      'iterations: same coordinates, Hi-C restraints and seeds as that GPU step), full demo protocol, '
+                      'fp64 C restatement, one structure per thread, %.1f s' % (n, args.warmup, dt)}
 
 
-def cpu_baseline_c(args, it, inp, nthreads):
+def cpu_baseline_c(args, it, inp, snap, warmup):
     """The fp64 C restatement (oracle/mstep_ref.c, kind 'port') on a bounded sample of
-    config C: one 200 kb structure per thread, same initial coordinates and Hi-C
-    restraints as the GPU's first step, the demo protocol with every MD step count
+    config C: one 200 kb structure per thread at the state of the first timed step
+    (coordinates, Hi-C restraints, seeds), the demo protocol with every MD step count
     scaled by args.c_cpu_scale (the stage mix kept), timed once with and once without
     the MD stages; the MD part is extrapolated to the full protocol and the CG part
     added as measured: t = (t_sample - t_cg) / scale + t_cg per structure."""
     import oracle
     from igm_amd import model as M
     from igm_amd._lib import bond_dtype
-    n = min(nthreads, it.S_local)
-    ptr = it.hic_ptr.cpu().numpy()
-    bonds = it.hic_bonds.cpu().numpy().view(bond_dtype)
+    nth, avail = host_threads(args)
+    ptr, bonds, xall, step_no = step_restraints(it, snap)
+    bonds = bonds.view(bond_dtype)
+    n = min(nth, it.S_local)
     sptr = ptr[:n + 1].copy()
     sb = bonds[:sptr[-1]].copy()
-    x = inp['xyz'][:n].copy()
-    seeds = M.lammps_seeds(it.seed, np.arange(n), 0)
+    x = np.ascontiguousarray(xall[:n])
+    seeds = M.lammps_seeds(it.seed, it.sids[:n], step_no)
     proto = json.loads(json.dumps(syn_protocol()))
     cap = proto['custom_annealing_protocol']
     sc = args.c_cpu_scale
@@ -138,11 +178,11 @@ def cpu_baseline_c(args, it, inp, nthreads):
     oracle.mstep_run(prm, x.copy(), inp['atoms'].radii, inp['atoms'].flags, inp['poly'], sptr, sb, seeds, nthreads=n)
     t_cg = time.perf_counter() - t0
     t_full = max(t_sample - t_cg, 0.0) / sc + t_cg
-    return {'value': n / t_full, 'unit': 'structures/s', 'cores': n, 'kind': 'port',
-            'sample': '%d structures of config C (200 kb, same initial coordinates and Hi-C restraints as GPU step 0), '
-                      'fp64 C restatement, one structure per thread; demo protocol MD steps x%g: %.1f s, CG alone '
-                      '%.1f s, extrapolated to the full protocol %.0f s per %d structures' % (n, sc, t_sample, t_cg,
-                                                                                          t_full, n)}
+    return {'value': n / t_full, 'unit': 'structures/s', 'cores': n, 'host_cpus_visible': avail, 'kind': 'port',
+            'sample': '%d structures of config C at the state of the first timed step (after %d warmup A/M '
+                      'iterations: same coordinates, Hi-C restraints and seeds), fp64 C restatement, one structure '
+                      'per thread; demo protocol MD steps x%g: %.1f s, CG alone %.1f s, extrapolated to the full '
+                      'protocol %.0f s per %d structures' % (n, warmup, sc, t_sample, t_cg, t_full, n)}
 
 
 def syn_protocol():
@@ -169,63 +209,82 @@ def cpu_baseline_astep(args, it, nthreads, npairs=4000):
             'sample': '%d seeded pairs of the same list, %d structures, %.2f s' % (len(sub), it.S_total, dt)}
 
 
-def bench_config_c(args, dev, ctx_threads):
-    """SURVEY 8(d) config C (BASELINE.json configs[2]): 200 kb diploid, the 125-structure
-    shard one GPU owns at 8 GPUs, Hi-C sigma 0.01, full demo protocol, inputs resident
-    in HBM; c_warmup + c_steps A/M iterations on this GPU alone.  Roofline of the
-    population engine: SURVEY 8(d)'s algorithmic bytes per force evaluation per
-    structure (76 N + 16 B) times the evaluations of the anneal, over the anneal's
-    HIP-event time (the five pop_* kernels of every MD step)."""
+def bench_config_c(args, dev, world, rank, local):
+    """SURVEY 8(d) config C (BASELINE.json configs[2], the metric's workload): 200 kb
+    diploid, Hi-C sigma 0.01, full demo protocol, inputs resident in HBM.  The
+    population of args.c_total structures is split over the ranks (STRONG scaling:
+    c_total / world structures per GPU; at 8 GPUs the 125-structure shards of
+    pop=1000), the A-step over the whole population through the RCCL all-gather;
+    c_warmup + c_steps A/M iterations, timed between barriers, max over ranks.
+    Roofline of the population engine: SURVEY 8(d)'s algorithmic bytes per force
+    evaluation per structure (76 N + 16 B) times the evaluations of the anneal, over
+    the anneal's HIP-event time (the pop_* kernels of every MD step)."""
     import torch
+    import torch.distributed as dist
     from igm_amd.pipeline import AMIteration
+    total = args.c_total
+    if total % world:
+        raise ValueError('config C population %d does not split over %d ranks' % (total, world))
+    per = total // world
     ca = argparse.Namespace(**vars(args))
-    ca.config, ca.nstruct, ca.sigma = 'C', 125, 0.01  # protocol_scale: 1.0 for the metric
-    inp = build_inputs(ca, 0)
+    ca.config, ca.nstruct, ca.sigma = 'C', per, 0.01  # protocol_scale: 1.0 for the metric
+    inp = build_inputs(ca, rank)
     pop = inp['pop']
     it = AMIteration(dev, inp['xyz'], inp['atoms'], inp['chrom'], pop['copy_ptr'], pop['copy_idx'], inp['pairs'],
-                     inp['prm'], inp['poly'], first_sid=0, rank=0, world=1)
-    cpu = None
-    if args.c_cpu_scale > 0:
-        it.astep()
-        it.select()
+                     inp['prm'], inp['poly'], first_sid=inp['first'], rank=rank, world=world)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
         torch.cuda.synchronize(dev)
-        cpu = cpu_baseline_c(args, it, inp, ctx_threads)
-        it.xyz.copy_(torch.from_numpy(inp['xyz']).to(dev))
-        it.pairs.copy_(torch.from_numpy(np.ascontiguousarray(inp['pairs']).view(np.uint8)).to(dev))
+
     for _ in range(args.c_warmup):
         it.step()
-    torch.cuda.synchronize(dev)
-    anneal_ms, bytes_launch = [], []
+    barrier()
+    want_cpu = args.c_cpu_scale > 0 and world == 1 and rank == 0
+    snap = it.snapshot() if want_cpu else None
+    anneal_ms, bytes_launch, steps = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.c_steps):
-        tm = it.step()
+        steps.append(it.step())
         anneal_ms.append(it.ctx.kernel_ms('anneal'))
         bytes_launch.append(it.algorithmic_anneal_bytes())
-    torch.cuda.synchronize(dev)
+    barrier()
     dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    kms = {k: it.ctx.kernel_ms(k) for k in ('cg', 'actdist', 'actdist_select', 'hic_select', 'violations')}
+    score = it.violation_score()
+    info = it.info_host()
+    nrows, nbonds, S_local = int(it.nrows), it.nbonds, it.S_local
+    cpu = cpu_baseline_c(args, it, inp, snap, args.c_warmup) if want_cpu else None
     a_ms = float(np.mean(anneal_ms))
     achieved = float(np.mean(bytes_launch)) / (a_ms * 1e-3) / 1e9
-    info = it.info_host()
     traffic, traffic_src = measured_traffic('C')
+    tm = steps[-1]
     out = {
-        'metric': 'M-step structures/sec + A/M iteration wall-time, 200 kb diploid, the 125-structure shard of '
-                  'pop=1000 at 8 GPUs (configs[2]) on 1 GPU',
-        'value': it.S_local * args.c_steps / dt, 'unit': 'structures/s', 'steps': args.c_steps,
-        'warmup': args.c_warmup, 'ms_per_step': 1000.0 * dt / args.c_steps,
-        'config': {'workload': 'C: 200 kb diploid (29 838 beads), Hi-C only, 125 structures, demo protocol',
-                   'sigma': 0.01, 'npairs': int(it.npairs_total)},
-        'roofline': {'bound': 'hbm', 'kernel': 'population engine (pop_integrate, pop_sort, pop_permute, pop_fill, '
-                                               'pop_force per MD step)',
+        'metric': 'M-step structures/sec + A/M iteration wall-time, 200 kb diploid pop=%d (configs[2]) on %d GPU%s'
+                  % (total, world, 's' if world > 1 else ''),
+        'value': total * args.c_steps / dt, 'unit': 'structures/s', 'n_gpus': world, 'steps': args.c_steps,
+        'warmup': args.c_warmup, 'ms_per_step': 1000.0 * dt / args.c_steps, 'scaling': 'strong',
+        'config': {'workload': 'C: 200 kb diploid (29 838 beads), Hi-C only, pop=%d, %d structures per GPU, demo '
+                               'protocol' % (total, per),
+                   'nstruct_total': total, 'nstruct_per_gpu': per, 'sigma': 0.01, 'npairs': int(it.npairs_total),
+                   'parallelism': 'structures sharded over %d ranks, A-step pair-sharded after an RCCL all-gather'
+                                  % world if world > 1 else 'one GPU'},
+        'roofline': {'bound': 'hbm', 'kernel': 'population engine (pop_* kernels of every MD step)',
                      'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                      'traffic': traffic, 'traffic_source': traffic_src,
                      'algorithmic_bytes_per_launch': float(np.mean(bytes_launch)), 'avg_launch_ms': a_ms},
         'cpu_baseline': cpu,
         'breakdown': {'astep_ms': 1000 * tm['astep_s'], 'mstep_ms': 1000 * tm['mstep_s'], 'anneal_ms': a_ms,
-                      'cg_ms': it.ctx.kernel_ms('cg'), 'actdist_ms': it.ctx.kernel_ms('actdist'),
-                      'hic_select_ms': it.ctx.kernel_ms('hic_select'),
-                      'violation_score': it.violation_score(),
+                      'cg_ms': kms['cg'], 'actdist_ms': kms['actdist'], 'actdist_select_ms': kms['actdist_select'],
+                      'hic_select_ms': kms['hic_select'], 'violations_ms': kms['violations'],
+                      'violation_score': score,
                       'median_final_energy_per_bead': float(np.median(info['final_energy'])) / inp['atoms'].nbead,
-                      'rows': int(it.nrows), 'hic_bonds_per_struct': it.nbonds / it.S_local,
+                      'rows': nrows, 'hic_bonds_per_struct': nbonds / S_local,
                       'mean_rebuilds': float(np.mean(info['nrebuild']))},
         'excludes': 'host pair enumeration (select_pairs) and file I/O: inputs resident in HBM',
     }
@@ -312,12 +371,12 @@ def measured_traffic(config):
 
 
 def measured_issue(config):
-    """VALU-issue roofline of the anneal kernel from the committed SQ counter passes
-    (scripts/gpu_r02.sh -> profiles/<round>/sq*.txt), kept in bench_issue.json: the
-    fraction of each SIMD's cycles spent issuing VALU instructions (a wave64 VALU op
-    occupies a 16-lane SIMD for 4 cycles): SQ_INSTS_VALU * SQ_WAVES / (SIMDs *
-    SQ_WAVE_CYCLES) with every wave resident for the whole launch.  The anneal kernel
-    keeps its structure in LDS, so this -- not HBM -- is its binding roofline."""
+    """VALU-pipe fraction of the anneal kernel from the committed SQ counter passes
+    (scripts/make_issue.py over profiles/<round>/sq*.txt), kept in bench_issue.json:
+    the fraction of each SIMD-32's cycles its VALU pipe is busy (2 cycles per wave64
+    VALU instruction; SQ_WAVE_CYCLES in quad-cycles), beside the wait and LDS
+    bank-conflict shares.  The anneal kernel keeps its structure in LDS, so these --
+    not HBM bytes -- say what binds it."""
     path = os.path.join(ROOT, 'bench_issue.json')
     if not os.path.exists(path):
         return None
@@ -347,19 +406,11 @@ def main():
             dist.barrier(device_ids=[local])
         torch.cuda.synchronize(dev)
 
-    cpu = None
-    if args.cpu_sample > 0 and world == 1 and rank == 0:
-        # restraints of the initial coordinates for the baseline sample (same as GPU step 0)
-        it.astep()
-        it.select()
-        torch.cuda.synchronize(dev)
-        cpu = cpu_baseline(args, it, inp)
-        it.xyz.copy_(torch.from_numpy(inp['xyz']).to(dev))
-        it.pairs.copy_(torch.from_numpy(np.ascontiguousarray(inp['pairs'][it.pair_lo:it.pair_hi]).view(np.uint8))
-                       .to(dev))
     for _ in range(args.warmup):
         it.step()
     barrier()
+    want_cpu = args.cpu_sample > 0 and world == 1 and rank == 0
+    snap = it.snapshot() if want_cpu else None  # the first timed step's input state
     anneal_ms, bytes_launch, astep_s, mstep_s = [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -370,22 +421,27 @@ def main():
         mstep_s.append(tm['mstep_s'])
     barrier()
     dt = time.perf_counter() - t0
-    kms = {k: it.ctx.kernel_ms(k) for k in ('cg', 'actdist', 'hic_select', 'violations')}  # before the C block
+    kms = {k: it.ctx.kernel_ms(k) for k in ('cg', 'actdist', 'actdist_select', 'hic_select', 'violations')}
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    de = cblock = astep_cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        astep_cpu = cpu_baseline_astep(args, it, args.cpu_threads)
-    if rank == 0 and world == 1 and not args.no_de:  # the N=1 line carries it; scaling runs stay lean
-        de = bench_asteps_de(args, it.ctx)
     score = it.violation_score()
     info = it.info_host()
-    if rank == 0 and world == 1 and args.config == 'B' and not args.no_c:
-        cblock = bench_config_c(args, dev, args.cpu_threads)
+    nrows, nbonds, S_local, npairs, npairs_total = int(it.nrows), it.nbonds, it.S_local, it.npairs, it.npairs_total
+    de = cblock = astep_cpu = cpu = None
+    if want_cpu:
+        nth, _ = host_threads(args)
+        astep_cpu = cpu_baseline_astep(args, it, nth)
+        cpu = cpu_baseline(args, it, inp, snap)
+    if rank == 0 and world == 1 and not args.no_de:  # the N=1 line carries it; scaling runs stay lean
+        de = bench_asteps_de(args, it.ctx)
+    del it, snap
+    torch.cuda.empty_cache()
+    if args.config == 'B' and not args.no_c:  # every rank: the 200 kb pop=c_total population, strong split
+        cblock = bench_config_c(args, dev, world, rank, local)
     ms_per_step = 1000.0 * dt / max(args.steps, 1)
-    total = it.S_local * world
+    total = S_local * world
     value = total * args.steps / dt
     a_ms = float(np.mean(anneal_ms)) if anneal_ms else float('nan')
     achieved = float(np.mean(bytes_launch)) / (a_ms * 1e-3) / 1e9 if anneal_ms else 0.0
@@ -404,8 +460,8 @@ def main():
                            'B: 2 Mb diploid (3008 beads)' if args.config == 'B' else 'C: 200 kb diploid (29 838 beads)',
                            args.nstruct, '' if args.protocol_scale == 1.0 else
                            ' x%g (NOT the metric)' % args.protocol_scale),
-                       'nstruct_per_gpu': it.S_local, 'nstruct_total': total, 'sigma': args.sigma,
-                       'npairs': int(it.npairs_total), 'parallelism': 'structures sharded, A-step pair-sharded'},
+                       'nstruct_per_gpu': S_local, 'nstruct_total': total, 'sigma': args.sigma,
+                       'npairs': int(npairs_total), 'parallelism': 'structures sharded, A-step pair-sharded'},
             'roofline': {'bound': 'hbm', 'kernel': 'anneal_kernel' if args.config == 'B' else
                          'population engine (pop_integrate, pop_sort, pop_permute, pop_fill, pop_force per MD step)',
                          'achieved': achieved, 'peak': HBM_PEAK_GBS,
@@ -416,21 +472,19 @@ def main():
             'roofline_issue': measured_issue(args.config),
             'cpu_baseline': cpu,
             'cpu_baseline_astep': astep_cpu,
-            'astep_pairs_per_s': float(it.npairs) / (kms['actdist'] * 1e-3),
+            'astep_pairs_per_s': float(npairs) / (kms['actdist'] * 1e-3),
             'config_C': cblock,
             'asteps_DE': de,
             'breakdown': {'astep_ms': 1000 * float(np.mean(astep_s)), 'mstep_ms': 1000 * float(np.mean(mstep_s)),
                           'anneal_ms': a_ms, 'cg_ms': kms['cg'],
-                          'actdist_ms': kms['actdist'], 'hic_select_ms': kms['hic_select'],
-                          'violations_ms': kms['violations'],
+                          'actdist_ms': kms['actdist'], 'actdist_select_ms': kms['actdist_select'],
+                          'hic_select_ms': kms['hic_select'], 'violations_ms': kms['violations'],
                           'violation_score': score, 'median_final_energy_per_bead':
                               float(np.median(info['final_energy'])) / inp['atoms'].nbead,
-                          'rows': int(it.nrows), 'hic_bonds_per_struct': it.nbonds / it.S_local,
+                          'rows': nrows, 'hic_bonds_per_struct': nbonds / S_local,
                           'mean_rebuilds': float(np.mean(info['nrebuild']))},
             'excludes': 'host pair enumeration (select_pairs) and file I/O: inputs resident in HBM',
         }
-        if os.environ.get('IGM_PROF'):
-            line['profile'] = it.ctx.mstep_profile()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

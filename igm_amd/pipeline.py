@@ -314,6 +314,17 @@ class AMIteration(object):
             self.pairs[:self.npairs * pair_dtype.itemsize].copy_(torch.from_numpy(pairs.view(np.uint8)))
         self.step_no = step_no
 
+    # ------------------------------------------------------------------ snapshots
+    def snapshot(self):
+        """the loop state one step starts from (device copies): structures, pair list
+        with its plast, step counter"""
+        return {'xyz': self.xyz.clone(), 'pairs': self.pairs.clone(), 'step_no': self.step_no}
+
+    def load_snapshot(self, snap):
+        self.xyz.copy_(snap['xyz'])
+        self.pairs.copy_(snap['pairs'])
+        self.step_no = snap['step_no']
+
     def info_host(self):
         return self.info.cpu().numpy().view(optinfo_dtype)
 

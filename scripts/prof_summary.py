@@ -55,6 +55,19 @@ def busy_union(db, pattern='pop_'):
             'mean_concurrency': tot / union, 'launches': len(iv)}
 
 
+def launches(db, pattern):
+    """every launch of the kernels matching `pattern` in dispatch order: (start offset
+    from the first, duration) in ms -- the per-launch durations the bench's HIP events
+    are compared with (launch 1 of a bench run is the warmup)"""
+    c = sqlite3.connect(db)
+    rows = list(c.execute('select name, start, end from kernels where name like ? order by start',
+                          ('%' + pattern + '%',)))
+    if not rows:
+        return []
+    t0 = rows[0][1]
+    return [(short(n, 40), (a - t0) * 1e-6, (b - a) * 1e-6) for n, a, b in rows]
+
+
 def pmc(db):
     c = sqlite3.connect(db)
     q = ('select kernel_name, counter_name, count(*), sum(value), avg(end - start) from counters_collection '
@@ -72,6 +85,30 @@ def main(src, dst):
                 u = busy_union(db, pat)
                 if u:
                     f.write('# busy union of %s kernels: %s\n' % (pat, u))
+        with open(os.path.join(dst, 'anneal_launches.txt'), 'w') as f:
+            f.write('# per-launch durations, dispatch order (launch 1 = warmup of the bench run); %s\n'
+                    % os.path.basename(db))
+            for pat in ('anneal_kernel', 'cg_kernel', 'classify_kernel', 'actdist_kernel'):
+                for n, st, d in launches(db, pat):
+                    f.write('%-40s start %12.3f ms  duration %12.3f ms\n' % (n, st, d))
+            # the population engine: one anneal = the pop_* dispatches between two pop_load launches
+            c = sqlite3.connect(db)
+            rows = list(c.execute("select name, start, end from kernels where name like '%pop_%' order by start"))
+            spans, cur, last_load = [], None, None
+            for n, a, b in rows:
+                if 'pop_load' in n and (last_load is None or a - last_load > 1e6):  # the groups' loads: one anneal
+                    if cur:
+                        spans.append(cur)
+                    cur = [a, b]
+                elif cur:
+                    cur[1] = max(cur[1], b)
+                if 'pop_load' in n:
+                    last_load = a
+            if cur:
+                spans.append(cur)
+            for k, (a, b) in enumerate(spans):
+                f.write('population engine anneal %-15d span %12.3f ms (first pop_load .. last pop_* end)\n'
+                        % (k + 1, (b - a) * 1e-6))
     out = ['# PMC passes (one counter per rocprofv3 run). value_KB = rocprofv3 FETCH_SIZE/WRITE_SIZE summed over',
            '# the launches; hbm_bytes_per_launch = KB*1024/calls, FETCH_SIZE doubled (gfx950 correction).',
            '%-70s %-10s %6s %18s %22s %14s' % ('kernel', 'counter', 'calls', 'value_KB', 'hbm_bytes_per_launch',
