@@ -209,7 +209,18 @@ def cpu_baseline_astep(args, it, nthreads, npairs=4000):
             'sample': '%d seeded pairs of the same list, %d structures, %.2f s' % (len(sub), it.S_total, dt)}
 
 
-def bench_config_c(args, dev, world, rank, local):
+def max_over_ranks(dt, world, dev):
+    """the slowest rank's time (the contract's max over ranks)"""
+    if world == 1:
+        return dt
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if dist.get_backend() == 'nccl' else 'cpu')
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench_config_c(args, dev, world, rank, local, backend='nccl'):
     """SURVEY 8(d) config C (BASELINE.json configs[2], the metric's workload): 200 kb
     diploid, Hi-C sigma 0.01, full demo protocol, inputs resident in HBM.  The
     population of args.c_total structures is split over the ranks (STRONG scaling:
@@ -234,8 +245,9 @@ def bench_config_c(args, dev, world, rank, local):
                      inp['prm'], inp['poly'], first_sid=inp['first'], rank=rank, world=world)
 
     def barrier():
+        torch.cuda.synchronize(dev)
         if world > 1:
-            dist.barrier(device_ids=[local])
+            dist.barrier(device_ids=[local]) if backend == 'nccl' else dist.barrier()
         torch.cuda.synchronize(dev)
 
     for _ in range(args.c_warmup):
@@ -250,11 +262,7 @@ def bench_config_c(args, dev, world, rank, local):
         anneal_ms.append(it.ctx.kernel_ms('anneal'))
         bytes_launch.append(it.algorithmic_anneal_bytes())
     barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(time.perf_counter() - t0, world, dev)
     kms = {k: it.ctx.kernel_ms(k) for k in ('cg', 'actdist', 'actdist_select', 'hic_select', 'violations')}
     score = it.violation_score()
     info = it.info_host()
@@ -270,7 +278,8 @@ def bench_config_c(args, dev, world, rank, local):
         'value': total * args.c_steps / dt, 'unit': 'structures/s', 'n_gpus': world, 'steps': args.c_steps,
         'warmup': args.c_warmup, 'ms_per_step': 1000.0 * dt / args.c_steps, 'scaling': 'strong',
         'config': {'workload': 'C: 200 kb diploid (29 838 beads), Hi-C only, pop=%d, %d structures per GPU, demo '
-                               'protocol' % (total, per),
+                               'protocol%s' % (total, per, '' if args.protocol_scale == 1.0 else
+                                               ' x%g (NOT the metric)' % args.protocol_scale),
                    'nstruct_total': total, 'nstruct_per_gpu': per, 'sigma': 0.01, 'npairs': int(it.npairs_total),
                    'parallelism': 'structures sharded over %d ranks, A-step pair-sharded after an RCCL all-gather'
                                   % world if world > 1 else 'one GPU'},
@@ -391,8 +400,16 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # RCCL ('nccl') is the product path; IGM_BENCH_BACKEND=gloo rehearses the N > 1 code on
+    # one GPU (every rank on cuda:0, collectives host-staged) -- never a measurement
+    backend = os.environ.get('IGM_BENCH_BACKEND', 'nccl')
+    if backend != 'nccl':
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     from igm_amd.pipeline import AMIteration
@@ -402,8 +419,9 @@ def main():
                      inp['prm'], inp['poly'], first_sid=inp['first'], rank=rank, world=world)
 
     def barrier():
+        torch.cuda.synchronize(dev)
         if world > 1:
-            dist.barrier(device_ids=[local])
+            dist.barrier(device_ids=[local]) if backend == 'nccl' else dist.barrier()
         torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
@@ -422,10 +440,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     kms = {k: it.ctx.kernel_ms(k) for k in ('cg', 'actdist', 'actdist_select', 'hic_select', 'violations')}
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(dt, world, dev)
     score = it.violation_score()
     info = it.info_host()
     nrows, nbonds, S_local, npairs, npairs_total = int(it.nrows), it.nbonds, it.S_local, it.npairs, it.npairs_total
@@ -439,7 +454,7 @@ def main():
     del it, snap
     torch.cuda.empty_cache()
     if args.config == 'B' and not args.no_c:  # every rank: the 200 kb pop=c_total population, strong split
-        cblock = bench_config_c(args, dev, world, rank, local)
+        cblock = bench_config_c(args, dev, world, rank, local, backend)
     ms_per_step = 1000.0 * dt / max(args.steps, 1)
     total = S_local * world
     value = total * args.steps / dt
