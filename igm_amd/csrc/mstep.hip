@@ -938,6 +938,7 @@ struct AnnealArgs {
     int seg_steps[2 * IGM_MAX_STAGES];
     float seg_evf[2 * IGM_MAX_STAGES], seg_envf[2 * IGM_MAX_STAGES], seg_t0[2 * IGM_MAX_STAGES],
         seg_t1[2 * IGM_MAX_STAGES], seg_xmax[2 * IGM_MAX_STAGES];
+    float seg_skin[2 * IGM_MAX_STAGES];  // Verlet skin of every run (equal forces for any skin; see run_anneal)
     float dt, t_window, t_fraction;
 };
 
@@ -1082,7 +1083,12 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
             const float dtv = A.dt, dtf = 0.5f * A.dt;
             const float vlim = A.seg_xmax[seg] / dtv;
             const float vlimsq = vlim * vlim;
-            const float trig = 0.25f * A.P.skin * A.P.skin;
+            const float skin = A.seg_skin[seg];
+            const float trig = 0.25f * skin * skin;
+            const float cut_list = A.P.cut_list - A.P.skin + skin;
+            if (seg > 0 && skin != A.seg_skin[seg - 1])  // a new cut: rebuild at the run's setup step
+#pragma unroll
+                for (int b = 0; b < BPT; ++b) xb[b][0] = xb[b][1] = xb[b][2] = __int_as_float(0x7f800000);
             // ---- run nsteps: step 0 is Verlet::setup (forces only)
             for (int step = 0; step <= nsteps; ++step) {
                 int moved = 0;
@@ -1104,7 +1110,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                 }
                 if (__syncthreads_or(moved)) {  // neigh_modify every 1 check yes
                     const unsigned long long c0 = A.prof ? clock64() : 0;
-                    const unsigned long long cw = build_nlist_lds<NT>(natom, sm.pos, sm.L, A.P.cut_list, sm.r);
+                    const unsigned long long cw = build_nlist_lds<NT>(natom, sm.pos, sm.L, cut_list, sm.r);
                     if (A.prof) {
                         c_build += clock64() - c0;
                         c_walk += cw;
@@ -1395,6 +1401,10 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     float mm[6] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
     if (live) {
         if (S.integrate && !(__float_as_uint(v.w) & IGM_ATOM_FIXED)) {
+            // the final_integrate half-kick of the previous step: the force kernel only
+            // stores the force (its kinetic-energy partial used the same kicked velocity),
+            // so the kick is redone here, bit for bit, instead of storing v in between
+            if (S.rescale) kick_limit(v.x, v.y, v.z, f.x, f.y, f.z, S.dtf, S.vlim, S.vlimsq);
             v.x *= factor;
             v.y *= factor;
             v.z *= factor;
@@ -2103,8 +2113,9 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
         }
         B.frc[k] = make_float4(fx, fy, fz, 0.f);
         if (S.integrate && !(fl & IGM_ATOM_FIXED)) {
+            // final_integrate for the temperature only: the kicked velocity is not stored
+            // (the next integrate, or the run's finish, redoes the kick from v and f)
             kick_limit(v.x, v.y, v.z, fx, fy, fz, S.dtf, S.vlim, S.vlimsq);
-            B.vel[k] = v;
             ke = (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z);
         }
     }
@@ -2131,6 +2142,10 @@ __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S
     const PopBuf& B = A.buf[A.par[s]];
     const size_t k = (size_t)s * A.cm.ldn + i;
     float4 v = B.vel[k];
+    if (S.rescale && !(__float_as_uint(v.w) & IGM_ATOM_FIXED)) {  // the last step's final_integrate
+        const float4 f = B.frc[k];
+        kick_limit(v.x, v.y, v.z, f.x, f.y, f.z, S.dtf, S.vlim, S.vlimsq);
+    }
     v.x *= factor;
     v.y *= factor;
     v.z *= factor;
@@ -2150,6 +2165,13 @@ __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S
         forces_out[a * 3 + 1] = f.y;
         forces_out[a * 3 + 2] = f.z;
     }
+}
+
+// every structure of the engine rebuilds its list at the next step (a run whose Verlet
+// skin differs from the last build's)
+__global__ void pop_flag_all_kernel(PopArgs A, int fp) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < A.cm.nstruct) A.flag[fp][s] = 1;
 }
 
 __global__ void deg_max_kernel(const int* deg, size_t n, int* out) {
@@ -3302,7 +3324,32 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         }
     }
     long gbase = 0;  // steps of the earlier segments: the flag parity runs on across segments
+    // Verlet skin per run (tuning knob IGM_POP_SKIN_SEG = "f0,f1,..." in units of the
+    // largest radius; absent: the engine's skin for every run).  Any skin gives the same
+    // forces -- the list holds every pair within cut_list = 2 rmax + skin and is rebuilt
+    // once an atom moved skin / 2 -- so hot runs (frequent rebuilds) can trade longer
+    // lists for fewer rebuilds and cold ones the reverse.
+    std::vector<float> seg_skin(A.seg_skin, A.seg_skin + A.nseg);
+    if (const char* e = getenv("IGM_POP_SKIN_SEG")) {  // the population engine's own (tuning)
+        const float rmax = 0.5f * (pr.P.cut_list - pr.P.skin);
+        int k = 0;
+        for (const char* q = e; *q && k < A.nseg; ++k) {
+            seg_skin[k] = (float)atof(q) * rmax;
+            while (*q && *q != ',') ++q;
+            if (*q == ',') ++q;
+        }
+    }
+    float last_skin = pr.P.skin;
     for (int seg = 0; seg < A.nseg; ++seg) {
+        if (seg_skin[seg] != last_skin) {  // a new cut: every list is rebuilt at the run's setup step
+            for (int g = 0; g < ng; ++g) {
+                V[g].P.cut_list = V[g].P.cut_list - last_skin + seg_skin[seg];
+                V[g].P.skin = seg_skin[seg];
+                hipLaunchKernelGGL(pop_flag_all_kernel, dim3((g0[g + 1] - g0[g] + 255) / 256), dim3(256), 0, strm(g),
+                                   V[g], (int)(gbase & 1));
+            }
+            last_skin = seg_skin[seg];
+        }
         const float* vsrc = A.mode == 1 ? A.vel : A.vinit + (size_t)seg * n3;
         const size_t sstride = A.mode == 1 ? n3 : (size_t)A.nseg * n3;
         for (int g = 0; g < ng; ++g)
@@ -3314,7 +3361,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         st.dtf = 0.5f * A.dt;
         st.vlim = A.seg_xmax[seg] / A.dt;
         st.vlimsq = st.vlim * st.vlim;
-        st.trig = 0.25f * pr.P.skin * pr.P.skin;
+        st.trig = 0.25f * seg_skin[seg] * seg_skin[seg];
         st.nsteps = A.seg_steps[seg];
         st.t0 = A.seg_t0[seg];
         st.t1 = A.seg_t1[seg];
@@ -3424,6 +3471,20 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
             hipLaunchKernelGGL(velocity_kernel, dim3(n, pr.cm.nstruct), dim3(256), 0, c->stream, V);
             IGM_HIP_CHECK(c, hipGetLastError());
             A.vinit = (const float*)pv;
+        }
+    }
+    // Verlet skin per run: the engine's skin unless IGM_SKIN_SEG = "f0,f1,..." (units of
+    // the largest radius) sets one per run -- any skin gives the same forces (the list
+    // holds every pair within 2 rmax + skin and is rebuilt once an atom moved skin / 2),
+    // so hot runs can trade longer lists for fewer rebuilds and cold ones the reverse
+    for (int k = 0; k < A.nseg; ++k) A.seg_skin[k] = pr.P.skin;
+    if (const char* e = getenv("IGM_SKIN_SEG")) {
+        const float rmax = 0.5f * (pr.P.cut_list - pr.P.skin);
+        int k = 0;
+        for (const char* q = e; *q && k < A.nseg; ++k) {
+            A.seg_skin[k] = (float)atof(q) * rmax;
+            while (*q && *q != ',') ++q;
+            if (*q == ',') ++q;
         }
     }
     IGM_HIP_CHECK(c, hipMemsetAsync(pr.cm.work_counter, 0, sizeof(int), c->stream));
