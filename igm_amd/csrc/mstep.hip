@@ -462,8 +462,8 @@ __device__ __forceinline__ float4 lds_f4(const IGM_LDS igm_f4v* p, int i) {
 }
 
 template <int NT>
-__device__ __noinline__ unsigned long long build_nlist_lds(int natom, const float4* pos_g, NList<float, uint16_t> Lg,
-                                                           float cut_list, Red R) {
+__device__ __noinline__ unsigned long long build_nlist_lds(int natom, int nwalk, const float4* pos_g,
+                                                           NList<float, uint16_t> Lg, float cut_list, Red R) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     constexpr int NW = NT / 64;
     const IGM_LDS igm_f4v* pos = (const IGM_LDS igm_f4v*)pos_g;
@@ -619,13 +619,17 @@ __device__ __noinline__ unsigned long long build_nlist_lds(int natom, const floa
     // threads take the beads in cell order (lanes of a wave = neighbouring cells: their
     // 27-cell walks have similar run lengths and read neighbouring positions); the
     // non-bead atoms have empty lists
-    for (int a = t; a < natom; a += NT)
-        if (!(lds_f4(pos, a).w >= 0.0f)) nnb[a] = 0;
-    const int nsorted = (int)cell[ncell];
-    for (int qa = t; qa < nsorted; qa += NT) {
-        const int a = (int)sorted[qa];
+    // (a domain of the domain-decomposed engine, nwalk < natom, walks its owned atoms in
+    // id order -- chain order, also spatially coherent -- so no lane idles on a halo atom)
+    const bool by_cell = nwalk == natom;
+    if (by_cell)
+        for (int a = t; a < nwalk; a += NT)
+            if (!(lds_f4(pos, a).w >= 0.0f)) nnb[a] = 0;
+    const int nq = by_cell ? (int)cell[ncell] : nwalk;
+    for (int qa = t; qa < nq; qa += NT) {
+        const int a = by_cell ? (int)sorted[qa] : qa;
 #else
-    for (int a = t; a < natom; a += NT) {
+    for (int a = t; a < nwalk; a += NT) {
 #endif
         const float4 p0 = lds_f4(pos, a);
         int k = 0;
@@ -819,7 +823,7 @@ template <int U>
 __device__ __forceinline__ void atom_force_md(int s, int a, const float4& p0, uint32_t fl, const float4* pos,
                                               const NList<float, uint16_t>& L, float bx, float by, float bz,
                                               const BondView& B, const DevParams& P, float evf,
-                                              float envf, float& fx, float& fy, float& fz) {
+                                              float envf, float& fx, float& fy, float& fz, int amax) {
     fx = fy = fz = 0.0f;
     const float xi = p0.x, yi = p0.y, zi = p0.z, ri = p0.w;
     double unused = 0.0;
@@ -831,7 +835,6 @@ __device__ __forceinline__ void atom_force_md(int s, int a, const float4& p0, ui
             // slots k0..k0+U-1 are always readable (LDS: kl is a multiple of U; HBM: the
             // overflow regions carry U-1 slack slots); a slot past n holds a stale or
             // scratch value, clamped to a valid atom, its bit cleared after the pass
-            const int amax = P.natom - 1;
             const int n1 = nn < L.kl ? nn : L.kl;
             const uint16_t* ll = L.lell + a;
             const int ls = __builtin_amdgcn_readfirstlane(L.lstride);  // uniform: scalar slot offsets
@@ -1110,7 +1113,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                 }
                 if (__syncthreads_or(moved)) {  // neigh_modify every 1 check yes
                     const unsigned long long c0 = A.prof ? clock64() : 0;
-                    const unsigned long long cw = build_nlist_lds<NT>(natom, sm.pos, sm.L, cut_list, sm.r);
+                    const unsigned long long cw = build_nlist_lds<NT>(natom, natom, sm.pos, sm.L, cut_list, sm.r);
                     if (A.prof) {
                         c_build += clock64() - c0;
                         c_walk += cw;
@@ -1139,7 +1142,8 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                         const uint32_t fla = ((f5 & 1u) ? IGM_ATOM_FIXED : 0u) | ((f5 >> 1) << 4);
                         atom_force_md<kLdsPairBatch>(s, a, sm.pos[a], fla, sm.pos,
                                                      sm.L, pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
-                                                     pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz);
+                                                     pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz,
+                                                     natom - 1);
 #pragma unroll
                         for (int i = 0; i < BPT; ++i)
                             if (b == i) {
@@ -2182,6 +2186,8 @@ __global__ void deg_max_kernel(const int* deg, size_t n, int* out) {
     for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
     if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
+
+#include "mstep_dd.h"
 
 // 'velocity nonfixed create T seed' (dist uniform, loop all, mom yes) for every
 // structure and segment: RanPark draws in atom-id order, momentum zeroed, scaled
@@ -3404,6 +3410,183 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     return IGM_OK;
 }
 
+// The domain-decomposed engine (mstep_dd.h) for a batch of structures too large for
+// one CU's LDS.  Sets *fell when it does not apply (LDS layout, occupancy) or when the
+// launch aborted (a domain past its capacity, a barrier past its time limit): the
+// caller then runs the multi-kernel population engine on the restored inputs.
+int run_anneal_dd(igm_ctx* c, const Prepared& pr, const AnnealArgs& A, int kmin_retry, bool* fell) {
+    *fell = true;
+    const int S = pr.cm.nstruct, N = pr.cm.natom;
+    if (A.nseg == 0) return IGM_OK;
+    const int cus = c->num_cus;
+    // Shape: BPT atoms per thread (2 or 3) and K domains per structure, every domain
+    // within 93 % of its owned capacity and its expected resident set within the
+    // resident capacity (measured halo shares on annealed 200 kb structures: 43 % of the
+    // owned atoms at K = 12, 59 % at 16, 75 % at 24; the largest domain's resident set
+    // ~1.35x the mean).  Modelled time: rounds of slots x rounds of 1024 owned atoms per
+    // step x a halo term growing with K.  29 838 atoms, 125 structures: BPT 2, K 16
+    // (8 rounds x 2).
+    int K = 0, bpt = 0, nt = 1024;
+    int want_k = 0, want_b = 0;
+    if (const char* e = getenv("IGM_DD_K")) want_k = atoi(e);
+    if (kmin_retry > 0) want_k = std::min(kmin_retry, std::min(kDdMaxK, cus));
+    if (const char* e = getenv("IGM_DD_BPT")) want_b = atoi(e);
+    if (const char* e = getenv("IGM_DD_NT")) nt = atoi(e) == 768 ? 768 : 1024;
+    double best = 1e300;
+    for (int k = 1; k <= kDdMaxK && k <= cus; ++k) {
+        if (want_k && k != want_k) continue;
+        // the smallest shape that holds the domain (fewer atoms per thread leave the most
+        // LDS for the halo)
+        const int64_t need = ceil_div(N, k);
+        int b = 0;
+        for (int bb = 2; bb <= 4 && !b; ++bb)
+            if ((nt == 1024 ? bb <= 3 : bb >= 3) && need <= (int64_t)(0.93 * dd_own_cap(nt, bb))) b = bb;
+        if (want_b) b = need <= dd_own_cap(nt, want_b) ? want_b : 0;
+        if (b == 0 || !dd_lds_ok(N, nt, b)) continue;
+        // resident set: owned x (1 + halo share), the largest domain ~1.4x the mean
+        if (!want_k && (k > 24 || 1.4 * (double)need * (1.0 + 0.037 * k) > dd_res_cap(nt, b))) continue;
+        const int slots = std::min(cus / k, S);
+        if (slots < 1) break;
+        const double cost = (double)ceil_div(S, slots) * (double)ceil_div(need, nt) * (1.0 + 0.02 * k);
+        if (cost < best) {
+            best = cost;
+            K = k;
+            bpt = b;
+        }
+    }
+    if (K < 1 || bpt < 2 || ceil_div(N, K) > dd_own_cap(nt, bpt)) return IGM_OK;
+    auto kern = nt == 768 ? (bpt == 3 ? dd_anneal_kernel<768, 3> : dd_anneal_kernel<768, 4>)
+                          : (bpt == 2 ? dd_anneal_kernel<1024, 2> : dd_anneal_kernel<1024, 3>);
+    if (nt == 768 && bpt != 3 && bpt != 4) return IGM_OK;
+    const DdLds lay = carve_dd_lds(nullptr, N, nt, bpt);
+    const size_t lds = lay.bytes;
+    IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int per_cu = 0;
+    IGM_HIP_CHECK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, nt, lds));
+    if (per_cu < 1) return IGM_OK;
+    const int nslot = std::min(cus / K, S);
+    const int grid = nslot * K;
+    // the largest bond degree sizes the owned atoms' bond slots
+    void* pdm;
+    IGM_TRY(workspace(c, "dd_dmax", sizeof(int), &pdm));
+    IGM_HIP_CHECK(c, hipMemsetAsync(pdm, 0, sizeof(int), c->stream));
+    hipLaunchKernelGGL(deg_max_kernel, dim3(1024), dim3(256), 0, c->stream, pr.cm.bonds.deg, (size_t)S * N, (int*)pdm);
+    int dmax = 0;
+    IGM_HIP_CHECK(c, hipMemcpyAsync(&dmax, pdm, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    DdArgs D;
+    memset(&D, 0, sizeof(D));
+    D.A = A;
+    D.K = K;
+    D.nslot = nslot;
+    D.bdmax = dmax > 0 ? dmax : 1;
+    D.kg = std::max(pr.cm.kcap - kLdsListSlots, 4);
+    D.gstride = ((size_t)dd_own_cap(nt, bpt) * D.kg * 2 + 64 * 2 * IGM_PAIR_BATCH + 255) & ~size_t(255);
+    const char* te = getenv("IGM_DD_TOL");
+    D.tol = te ? (float)atof(te) : 0.08f;
+    int wc_khz = 0;
+    IGM_HIP_CHECK(c, hipDeviceGetAttribute(&wc_khz, hipDeviceAttributeWallClockRate, c->device));
+    D.tmo = (long long)(wc_khz > 0 ? wc_khz : 100000) * 1000LL * 5;  // 5 s per barrier
+    void *px, *pv, *pk, *pvo, *psy, *pbe, *pge, *pst;
+    IGM_TRY(workspace(c, "dd_x", sizeof(float4) * (size_t)nslot * N, &px));
+    IGM_TRY(workspace(c, "dd_v", sizeof(float4) * (size_t)nslot * N, &pv));
+    IGM_TRY(workspace(c, "dd_ke", sizeof(unsigned long long) * (size_t)nslot * kDdMaxK, &pk));
+    IGM_TRY(workspace(c, "dd_vote", sizeof(int) * (size_t)nslot * kDdMaxK, &pvo));
+    const size_t sync_words = (size_t)(nslot + 1) * kDdSyncWords;  // slot counters, then the abort word
+    IGM_TRY(workspace(c, "dd_sync", sizeof(unsigned) * sync_words, &psy));
+    IGM_TRY(workspace(c, "dd_bell", sizeof(uint32_t) * (size_t)grid * dd_own_cap(nt, bpt) * D.bdmax, &pbe));
+    IGM_TRY(workspace(c, "dd_gell", D.gstride * (size_t)grid, &pge));
+    IGM_TRY(workspace(c, "dd_stats", sizeof(unsigned long long) * (8 + kDdProf), &pst));
+    D.X = (float4*)px;
+    D.V = (float4*)pv;
+    D.ke = (unsigned long long*)pk;
+    D.vote = (int*)pvo;
+    D.sync = (unsigned*)psy;
+    D.abort = (int*)((unsigned*)psy + (size_t)nslot * kDdSyncWords);
+    D.bell = (uint32_t*)pbe;
+    D.gell = (unsigned char*)pge;
+    D.stats = (unsigned long long*)pst;
+    const bool dprof = getenv("IGM_DD_PROF") != nullptr;
+    D.prof = dprof ? (unsigned long long*)pst + 8 : nullptr;
+    IGM_HIP_CHECK(c, hipMemsetAsync(psy, 0, sizeof(unsigned) * sync_words, c->stream));
+    IGM_HIP_CHECK(c, hipMemsetAsync(pst, 0, sizeof(unsigned long long) * (8 + kDdProf), c->stream));
+    // inputs kept for a fallback run
+    const size_t n3 = (size_t)S * N * 3;
+    void *px0, *pv0 = nullptr;
+    IGM_TRY(workspace(c, "dd_x0", sizeof(float) * n3, &px0));
+    IGM_HIP_CHECK(c, hipMemcpyAsync(px0, A.xyz, sizeof(float) * n3, hipMemcpyDeviceToDevice, c->stream));
+    if (A.mode == 1) {
+        IGM_TRY(workspace(c, "dd_v0", sizeof(float) * n3, &pv0));
+        IGM_HIP_CHECK(c, hipMemcpyAsync(pv0, A.vel, sizeof(float) * n3, hipMemcpyDeviceToDevice, c->stream));
+    }
+    {
+        Timed tm(c, "anneal");
+        void* args[] = {&D};
+        const hipError_t e =
+            hipLaunchCooperativeKernel((const void*)kern, dim3(grid), dim3(nt), args, (unsigned)lds, c->stream);
+        if (e == hipErrorCooperativeLaunchTooLarge) {
+            (void)hipGetLastError();
+            return IGM_OK;
+        }
+        IGM_HIP_CHECK(c, e);
+    }
+    int ab = 0;
+    unsigned long long st[8 + kDdProf];
+    IGM_HIP_CHECK(c, hipMemcpyAsync(&ab, D.abort, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    IGM_HIP_CHECK(c, hipMemcpyAsync(st, pst, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    c->dd_stats[0] = K;
+    c->dd_stats[1] = nslot;
+    for (int k = 0; k < 4; ++k) c->dd_stats[2 + k] = (long long)st[k];
+    c->dd_stats[6] = ab;
+    if (getenv("IGM_DD_VERBOSE"))
+        fprintf(stderr,
+                "[igm dd] NT=%d BPT=%d K=%d slots=%d builds=%llu recuts=%llu max_res=%llu max_own=%llu max_geo=%llu "
+                "mean_res=%.0f mean_own=%.0f mean_geo=%.0f abort=%d\n",
+                nt, bpt, K, nslot, st[0], st[1], st[2], st[3], st[4], st[5] / (double)std::max(st[0], 1ull),
+                st[6] / (double)std::max(st[0], 1ull), st[7] / (double)std::max(st[0], 1ull), ab);
+    if (dprof) {  // per-workgroup mean, microseconds (wall clock)
+        const double us = 1e3 / (double)(wc_khz > 0 ? wc_khz : 100000), nw = (double)grid;
+        const char* nm[12] = {"integrate", "barA", "handover", "scan", "recut", "bonds", "list", "halo", "force",
+                              "barB", "steps", "builds"};
+        fprintf(stderr, "[igm dd prof] per workgroup:");
+        for (int k = 0; k < 12; ++k)
+            fprintf(stderr, " %s=%.1f%s", nm[k], st[8 + k] * (k < 10 ? us : 1.0) / nw, k < 10 ? "us" : "");
+        fprintf(stderr, "\n");
+    }
+    if (ab) {  // restore the inputs: the caller reruns the batch
+        IGM_HIP_CHECK(c, hipMemcpyAsync(A.xyz, px0, sizeof(float) * n3, hipMemcpyDeviceToDevice, c->stream));
+        if (A.mode == 1)
+            IGM_HIP_CHECK(c, hipMemcpyAsync(A.vel, pv0, sizeof(float) * n3, hipMemcpyDeviceToDevice, c->stream));
+        return IGM_OK;
+    }
+    *fell = false;
+    return IGM_OK;
+}
+
+// HBM-size structures: the multi-kernel population engine, or with params flag
+// IGM_MSTEP_ENGINE_DD (tuning: IGM_POP_ENGINE=dd) the domain-decomposed engine, which
+// falls back to the former when it does not apply or aborts.  (Measured on config C,
+// full demo protocol, 125 structures: population engine 16.1 s, domain-decomposed
+// 31.3 s -- DESIGN.md section 7.)
+int run_anneal_big(igm_ctx* c, const Prepared& pr, const AnnealArgs& A, int32_t pflags) {
+    const char* e = getenv("IGM_POP_ENGINE");
+    const bool dd = (pflags & IGM_MSTEP_ENGINE_DD) || (e && !strcmp(e, "dd"));
+    c->dd_stats[6] = -1;
+    if (dd) {
+        bool fell = true;
+        IGM_TRY(run_anneal_dd(c, pr, A, 0, &fell));
+        if (!fell) return IGM_OK;
+        // a domain past its resident capacity (frustrated structures hold more halo):
+        // once more with more, smaller domains
+        if (c->dd_stats[6] == 1 && c->dd_stats[0] > 0 && c->dd_stats[0] < kDdMaxK) {
+            IGM_TRY(run_anneal_dd(c, pr, A, (int)std::min<long long>(kDdMaxK, c->dd_stats[0] + 8), &fell));
+            if (!fell) return IGM_OK;
+        }
+    }
+    return run_anneal_pop(c, pr, A);
+}
+
 int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, float* d_xyz, float* d_vel,
                const int* d_seeds, int* d_nreb, int mode, double seg_evf, double seg_envf, double t0, double t1,
                double xmax, int nsteps, float* d_forces = nullptr) {
@@ -3507,7 +3690,7 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
         IGM_HIP_CHECK(c, hipMemsetAsync(pp, 0, sizeof(unsigned long long) * 8, c->stream));
         A.prof = (unsigned long long*)pp;
     }
-    if (pr.big) return run_anneal_pop(c, pr, A);
+    if (pr.big) return run_anneal_big(c, pr, A, prm->flags);
     LaunchCfg cfg;
     if (!lds_fits(pr.cm.natom, &cfg)) return fail(c, IGM_E_UNSUPPORTED, "no LDS configuration");
     IGM_DISPATCH_ALL({
@@ -3744,5 +3927,11 @@ extern "C" int igm_mstep_last_profile(igm_ctx* c, unsigned long long* out) {
     IGM_HIP_CHECK(c, hipMemcpyAsync(out, it->second.first, sizeof(unsigned long long) * 6, hipMemcpyDeviceToHost,
                                     c->stream));
     IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return IGM_OK;
+}
+
+extern "C" int igm_mstep_engine_stats(igm_ctx* c, long long* out) {
+    if (!c || !out) return IGM_E_INVALID;
+    for (int k = 0; k < 8; ++k) out[k] = c->dd_stats[k];
     return IGM_OK;
 }
