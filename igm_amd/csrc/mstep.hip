@@ -1253,6 +1253,10 @@ constexpr int kPopListCap = IGM_POP_LIST_CAP;  // Verlet-list entries per slot (
 #define IGM_POP_FUSED 0
 #endif
 constexpr bool kPopFused = IGM_POP_FUSED != 0;
+#ifndef IGM_POP_OUTER_CAP
+#define IGM_POP_OUTER_CAP 80
+#endif
+constexpr int kPopOuterCap = IGM_POP_OUTER_CAP;  // outer-list entries per slot (two-level lists)
 constexpr int kPopListRow = kPopListCap + 2;  // u16 per LDS list row of the build (odd word stride)
 
 struct PopBuf {
@@ -1292,6 +1296,26 @@ struct PopArgs {
     const uint32_t* csr;  // entries: partner atom | type << 16 | lower << 31
     const int* coff;      // (B, natom + 1) row offsets within the structure
     const int64_t* cbase;  // (B) first entry of the structure
+    // Two-level lists (two != 0): the cell grid, the slot order and the OUTER list
+    // (cut_list = cut_in + the outer margin) are rebuilt only when an atom moved past
+    // half the margin since the last outer build; the inner list (cut_in, the list
+    // the force kernel reads) is re-filtered from the outer one at every other rebuild.
+    int two;
+    float cut_in;        // inner list cut (two-level), P.cut_list is then the outer one
+    float4* xo;          // (B, ldn) position of the slot at the last outer build
+    uint2* nlo;          // (B, nslice, kqo, 64) outer list quads
+    uint16_t* nnbo;      // (B, ldn) outer list length, or kNnbWalk
+    int kqo;
+    int* oflag[2];       // (B) outer margin exceeded, by step parity
+    int* flist2;         // (B) the structures whose inner list is rebuilt this step
+    int* nflag2;         // (1)
+};
+
+// one Verlet list of the engine (the inner one, or the outer one of two-level lists)
+struct PopList {
+    uint2* nl;
+    uint16_t* nnb;
+    int kq;
 };
 
 // XCD-aware block order for the kernels over every structure: the grid (padded to a
@@ -1326,10 +1350,15 @@ __global__ void __launch_bounds__(256) pop_csr_fill_kernel(Bonds Bd, int nstruct
 __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float* xyz) {
     const int lb = pop_block(), s = lb / A.nbs, a = (lb % A.nbs) * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
-    if (lb == 0 && threadIdx.x == 0) *A.nflag = 0;
+    if (lb == 0 && threadIdx.x == 0) {
+        *A.nflag = 0;
+        *A.nflag2 = 0;
+    }
     if (a == 0) {
         A.flag[0][s] = 1;  // the first step builds
         A.flag[1][s] = 0;
+        A.oflag[0][s] = 1;
+        A.oflag[1][s] = 0;
         A.nrebuild[s] = 0;
         A.par[s] = 0;
     }
@@ -1346,6 +1375,7 @@ __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float
     B.slot[i] = a;
     const float inf = __int_as_float(0x7f800000);
     A.xb[i] = make_float4(inf, inf, inf, 0.f);
+    if (A.two) A.xo[i] = make_float4(inf, inf, inf, 0.f);
 }
 
 // velocities of a run: 'velocity create' of segment seg (vsrc = vinit + seg stride) or
@@ -1362,6 +1392,7 @@ __global__ void __launch_bounds__(kPopBS) pop_setvel_kernel(PopArgs A, const flo
 
 struct PopStep {
     float dtv, dtf, vlim, vlimsq, trig;
+    float trig_out;   // two-level lists: (outer margin / 2)^2
     int integrate;    // 0: neighbour check only (run setup)
     int rescale;      // apply the temp/rescale of step `prev` first
     int prev, nsteps;
@@ -1400,8 +1431,9 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     float4 v = B.vel[k];
     const float4 f = B.frc[k];
     const float4 b = A.xb[k];
+    const float4 bo = A.two ? A.xo[k] : b;
     const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
-    int moved = 0;
+    int moved = 0, moved_o = 0;
     float mm[6] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
     if (live) {
         if (S.integrate && !(__float_as_uint(v.w) & IGM_ATOM_FIXED)) {
@@ -1422,6 +1454,8 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
         if (p.w >= 0.0f) {
             const float dx = p.x - b.x, dy = p.y - b.y, dz = p.z - b.z;
             moved = !(dx * dx + dy * dy + dz * dz <= S.trig);
+            const float ox = p.x - bo.x, oy = p.y - bo.y, oz = p.z - bo.z;
+            moved_o = !(ox * ox + oy * oy + oz * oz <= S.trig_out);
             mm[0] = -p.x;
             mm[1] = -p.y;
             mm[2] = -p.z;
@@ -1438,6 +1472,7 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
 #pragma unroll
         for (int d = 0; d < 6; ++d) red[(threadIdx.x >> 6) * 6 + d] = mm[d];
     if (__syncthreads_or(moved) && threadIdx.x == 0) atomicOr(&A.flag[S.fp][s], 1);
+    if (A.two && __syncthreads_or(moved_o) && threadIdx.x == 0) atomicOr(&A.oflag[S.fp][s], 1);
     if (threadIdx.x < 6) {
         float m = red[threadIdx.x];
 #pragma unroll
@@ -1465,6 +1500,10 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
     __shared__ int sn[3];
     const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (!A.flag[fp][s]) return;
+    if (A.two) {  // every rebuild re-filters the inner list; the outer one waits for its margin
+        if (t == 0) A.flist2[atomicAdd(A.nflag2, 1)] = s;
+        if (!A.oflag[fp][s]) return;
+    }
     const int N = A.cm.natom;
     const size_t base = (size_t)s * A.cm.ldn;
     const int p = A.par[s], q = p ^ 1;
@@ -1688,6 +1727,7 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     B.vel[k] = O.vel[o];
     // (no force: the force kernel of this step rewrites every slot's before any read)
     A.xb[k] = make_float4(x.x, x.y, x.z, 0.f);
+    if (A.two) A.xo[k] = make_float4(x.x, x.y, x.z, 0.f);
     if (!BONDS) return;
     // the atom's bonds (sorted adjacency of prepare()) with partners as slots
     const int nsl = A.cm.nslice;
@@ -1742,13 +1782,13 @@ __device__ __forceinline__ float4 pop_ld(__amdgpu_buffer_rsrc_t r, uint32_t j) {
 // thread's LDS row `row` (kPopListRow u16), padded to whole quads with the slot itself,
 // stored as quads to the global list and its length (or kNnbWalk) to nnb.  Returns
 // the number of entries (> kcap: the slot takes its pairs from the cell walk).
-__device__ __forceinline__ int pop_fill_slot(const PopArgs& A, int s, int i, size_t base, const float4* pos,
-                                             float4 p0, uint32_t* row) {
+__device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T, int s, int i, size_t base,
+                                             const float4* pos, float4 p0, uint32_t* row) {
     const float* gp = A.gp + (size_t)s * 8;
     const int* gn = A.gn + (size_t)s * 8;
     const int* cell = A.cell + (size_t)s * kPopCells;
     const int nx = gn[0], ny = gn[1], nz = gn[2];
-    const int kcap = 4 * A.kq;  // <= kPopListCap
+    const int kcap = 4 * T.kq;  // <= kPopListCap
     uint16_t* lst = reinterpret_cast<uint16_t*>(row);
     const float cut2 = A.P.cut_list * A.P.cut_list;
     int k = 0;
@@ -1798,11 +1838,11 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, int s, int i, siz
     for (int kk = k; kk < kcap && (kk & 3); ++kk) lst[kk] = (uint16_t)i;
     const int nlist = k <= kcap ? ((k + 3) & ~3) : 0;  // entries incl. the padding
     if (nlist > 0) {
-        uint64_t* out = reinterpret_cast<uint64_t*>(A.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * A.kq * 64 + (i & 63));
+        uint64_t* out = reinterpret_cast<uint64_t*>(T.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * T.kq * 64 + (i & 63));
 #pragma unroll 1
         for (int q = 0; q < nlist >> 2; ++q) out[(size_t)q * 64] = ((uint64_t)row[2 * q + 1] << 32) | row[2 * q];
     }
-    A.nnb[base + i] = (uint16_t)(k <= kcap ? k : kNnbWalk);
+    T.nnb[base + i] = (uint16_t)(k <= kcap ? k : kNnbWalk);
     return k;
 }
 
@@ -1814,8 +1854,9 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, int s, int i, siz
 // neither the block's whole neighbourhood range (~50 KB, 18 % slower) nor the union of
 // the slots its lists use (lists rewritten to union indices: this kernel +58 %, the
 // force kernel +9 %).
+template <int ROW>
 __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
-    __shared__ uint32_t lrow[kPopBS * kPopListRow / 2];
+    __shared__ uint32_t lrow[kPopBS * ROW / 2];
     const int kb = blockIdx.x / A.nbs;
     if (kb >= *A.nflag) return;  // an idle block (the structure was not flagged)
     const int s = A.flist[kb], blk = blockIdx.x % A.nbs, t = threadIdx.x, i = blk * kPopBS + t;
@@ -1823,10 +1864,72 @@ __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
     const size_t base = (size_t)s * A.cm.ldn;
     const float4* pos = A.buf[A.par[s]].pos + base;
     const float4 p0 = pos[i];
+    const PopList T = A.two ? PopList{A.nlo, A.nnbo, A.kqo} : PopList{A.nl, A.nnb, A.kq};
     if (p0.w >= 0.0f)
-        pop_fill_slot(A, s, i, base, pos, p0, lrow + t * (kPopListRow / 2));
+        pop_fill_slot(A, T, s, i, base, pos, p0, lrow + t * (ROW / 2));
     else
+        T.nnb[base + i] = 0;
+}
+
+// Two-level lists: the inner Verlet list (cut_in) of every slot of a structure whose
+// inner list is rebuilt this step, filtered from its outer list (no cell walk, no new
+// slot order); a slot whose outer list overflowed keeps the cell walk.  Same output
+// format as pop_fill_slot (quads of slot ids in the list's order, the last one padded
+// with the slot itself).
+__global__ void __launch_bounds__(kPopBS) pop_refilter_kernel(PopArgs A) {
+    __shared__ uint32_t lrow[kPopBS * kPopListRow / 2];
+    const int kb = blockIdx.x / A.nbs;
+    if (kb >= *A.nflag2) return;
+    const int s = A.flist2[kb], t = threadIdx.x, i = (blockIdx.x % A.nbs) * kPopBS + t;
+    if (i >= A.cm.natom) return;
+    const size_t base = (size_t)s * A.cm.ldn;
+    const float4* pos = A.buf[A.par[s]].pos + base;
+    const float4 p0 = pos[i];
+    A.xb[base + i] = make_float4(p0.x, p0.y, p0.z, 0.f);  // the inner build position
+    if (!(p0.w >= 0.0f)) {
         A.nnb[base + i] = 0;
+        return;
+    }
+    const int no = A.nnbo[base + i];
+    if (no == kNnbWalk) {
+        A.nnb[base + i] = kNnbWalk;
+        return;
+    }
+    uint32_t* row = lrow + t * (kPopListRow / 2);
+    uint16_t* lst = reinterpret_cast<uint16_t*>(row);
+    const int kcap = 4 * A.kq;
+    const float cut2 = A.cut_in * A.cut_in;
+    const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
+    const uint2* go = A.nlo + ((size_t)s * A.cm.nslice + (i >> 6)) * A.kqo * 64 + (i & 63);
+    int k = 0;
+    auto test = [&](uint32_t j) {
+        const float3 p = pop_ld3(rp, j);
+        const float dx = p0.x - p.x, dy = p0.y - p.y, dz = p0.z - p.z;
+        const bool in = j != (uint32_t)i && dx * dx + dy * dy + dz * dz < cut2;  // (the padding is the slot)
+        if (in && k < kcap) lst[k] = (uint16_t)j;
+        k += in ? 1 : 0;
+    };
+    const int nq = (no + 3) >> 2;
+    for (int q0 = 0; q0 < nq; q0 += 2) {  // two quads (8 candidates) in flight
+        const uint2 e0 = go[(size_t)q0 * 64];
+        const uint2 e1 = q0 + 1 < nq ? go[(size_t)(q0 + 1) * 64] : make_uint2(i * 0x10001u, i * 0x10001u);
+        test(e0.x & 0xffffu);
+        test(e0.x >> 16);
+        test(e0.y & 0xffffu);
+        test(e0.y >> 16);
+        test(e1.x & 0xffffu);
+        test(e1.x >> 16);
+        test(e1.y & 0xffffu);
+        test(e1.y >> 16);
+    }
+    for (int kk = k; kk < kcap && (kk & 3); ++kk) lst[kk] = (uint16_t)i;
+    const int nlist = k <= kcap ? ((k + 3) & ~3) : 0;
+    if (nlist > 0) {
+        uint64_t* out = reinterpret_cast<uint64_t*>(A.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * A.kq * 64 + (i & 63));
+#pragma unroll 1
+        for (int q = 0; q < nlist >> 2; ++q) out[(size_t)q * 64] = ((uint64_t)row[2 * q + 1] << 32) | row[2 * q];
+    }
+    A.nnb[base + i] = (uint16_t)(k <= kcap ? k : kNnbWalk);
 }
 
 // pair forces of a slot past the Verlet-list capacity: the 27 cells of the build-time
@@ -1930,7 +2033,9 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     };
     if (ri >= 0.0f) {
         if (nn == kNnbWalk) {
-            const float4 b = A.xb[base + i];
+            // the walk covers the cells around the position of the grid's build (with
+            // two-level lists the outer build: the cells hold the slots of that build)
+            const float4 b = (A.two ? A.xo : A.xb)[base + i];
             const float4 f = pop_walk_pairs(pos, A.cell + (size_t)s * kPopCells, A.gp + (size_t)s * 8,
                                             A.gn + (size_t)s * 8, b.x, b.y, b.z, i, p0, evfpi);
             fx = f.x;
@@ -2090,11 +2195,15 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
     __shared__ uint32_t lrow[FUSED ? kPopBS * kPopListRow / 2 : 1];
     const int lb = pop_block(), s = lb / A.nbs, blk = lb % A.nbs, i = blk * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
-    if (lb == 0 && threadIdx.x == 0) *A.nflag = 0;  // the build kernels of this step are done
+    if (lb == 0 && threadIdx.x == 0) {  // the build kernels of this step are done
+        *A.nflag = 0;
+        *A.nflag2 = 0;
+    }
     const int rebuilt = A.flag[S.fp][s];  // the structure's list is (was) rebuilt this step
     if (i == 0) {
         A.nrebuild[s] += rebuilt ? 1 : 0;
         A.flag[S.fp ^ 1][s] = 0;  // the next step's flags start clear
+        A.oflag[S.fp ^ 1][s] = 0;
     }
     const size_t base = (size_t)s * A.cm.ldn, k = base + i;
     const PopBuf& B = A.buf[A.par[s]];
@@ -2108,7 +2217,7 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
             const float4 p0 = B.pos[k];
             int nb = 0;
             if (p0.w >= 0.0f)
-                nb = pop_fill_slot(A, s, i, base, B.pos + base, p0, row);
+                nb = pop_fill_slot(A, PopList{A.nl, A.nnb, A.kq}, s, i, base, B.pos + base, p0, row);
             else
                 A.nnb[k] = 0;
             pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, row, nb);
@@ -2175,7 +2284,10 @@ __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S
 // skin differs from the last build's)
 __global__ void pop_flag_all_kernel(PopArgs A, int fp) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < A.cm.nstruct) A.flag[fp][s] = 1;
+    if (s < A.cm.nstruct) {
+        A.flag[fp][s] = 1;
+        A.oflag[fp][s] = 1;
+    }
 }
 
 __global__ void deg_max_kernel(const int* deg, size_t n, int* out) {
@@ -3164,8 +3276,17 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     V.bdeg = Q.bdeg + o;
     V.flag[0] = Q.flag[0] + s0;
     V.flag[1] = Q.flag[1] + s0;
+    V.oflag[0] = Q.oflag[0] + s0;
+    V.oflag[1] = Q.oflag[1] + s0;
     V.flist = Q.flist + s0;
+    V.flist2 = Q.flist2 + s0;
     V.nflag = Q.nflag + g;
+    V.nflag2 = Q.nflag + 32 + g;
+    if (Q.two) {
+        V.xo = Q.xo + o;
+        V.nlo = Q.nlo + (size_t)s0 * nsl * Q.kqo * 64;
+        V.nnbo = Q.nnbo + o;
+    }
     V.nrebuild = Q.nrebuild + s0;
     V.kep = Q.kep + (size_t)s0 * Q.nbs;
     V.bbp = Q.bbp + (size_t)s0 * Q.nbs * 6;
@@ -3224,6 +3345,31 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     IGM_TRY(workspace(c, "pop_bb", sizeof(float) * 6 * (size_t)S * Q.nbs, &pbb));
     void* pnr = A.nrebuild;
     if (!pnr) IGM_TRY(workspace(c, "pop_nreb", sizeof(int) * (size_t)S, &pnr));
+    // two-level lists: the outer margin in units of the largest radius (0: one level)
+    const float rmax0 = 0.5f * (pr.P.cut_list - pr.P.skin);
+    float margin = 0.0f;
+    if (const char* e = getenv("IGM_POP_OUTER")) margin = (float)atof(e) * rmax0;
+    if (kPopFused) margin = 0.0f;
+    Q.two = margin > 0.0f ? 1 : 0;
+    constexpr int kOuterRow = kPopOuterCap + 2;
+    {
+        void *pfl2, *pfli2;
+        IGM_TRY(workspace(c, "pop_oflag", sizeof(int) * 2 * (size_t)S, &pfl2));
+        IGM_TRY(workspace(c, "pop_flist2", sizeof(int) * (size_t)S, &pfli2));
+        Q.oflag[0] = (int*)pfl2;
+        Q.oflag[1] = (int*)pfl2 + S;
+        Q.flist2 = (int*)pfli2;
+        if (Q.two) {
+            void *pxo, *pnlo, *pnnbo;
+            Q.kqo = kPopOuterCap / 4;
+            IGM_TRY(workspace(c, "pop_xo", sizeof(float4) * SL, &pxo));
+            IGM_TRY(workspace(c, "pop_nlo", sizeof(uint2) * SL * Q.kqo, &pnlo));
+            IGM_TRY(workspace(c, "pop_nnbo", sizeof(uint16_t) * SL, &pnnbo));
+            Q.xo = (float4*)pxo;
+            Q.nlo = (uint2*)pnlo;
+            Q.nnbo = (uint16_t*)pnnbo;
+        }
+    }
     Q.par = (int*)ppar;
     Q.xb = (float4*)pxb;
     Q.nl = (uint2*)pnl;
@@ -3237,6 +3383,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.flag[1] = (int*)pfl + S;
     Q.flist = (int*)pfli;
     Q.nflag = (int*)pnf;
+    Q.nflag2 = (int*)pnf + 32;
     Q.kep = (double*)pke;
     Q.bbp = (float*)pbb;
     Q.nrebuild = (int*)pnr;
@@ -3347,9 +3494,10 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     }
     float last_skin = pr.P.skin;
     for (int seg = 0; seg < A.nseg; ++seg) {
-        if (seg_skin[seg] != last_skin) {  // a new cut: every list is rebuilt at the run's setup step
+        if (seg_skin[seg] != last_skin || seg == 0) {  // a new cut: every list is rebuilt at the run's setup step
             for (int g = 0; g < ng; ++g) {
-                V[g].P.cut_list = V[g].P.cut_list - last_skin + seg_skin[seg];
+                V[g].P.cut_list = 2.0f * rmax0 + seg_skin[seg] + margin;  // (two-level: the outer cut)
+                V[g].cut_in = 2.0f * rmax0 + seg_skin[seg];
                 V[g].P.skin = seg_skin[seg];
                 hipLaunchKernelGGL(pop_flag_all_kernel, dim3((g0[g + 1] - g0[g] + 255) / 256), dim3(256), 0, strm(g),
                                    V[g], (int)(gbase & 1));
@@ -3368,6 +3516,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         st.vlim = A.seg_xmax[seg] / A.dt;
         st.vlimsq = st.vlim * st.vlim;
         st.trig = 0.25f * seg_skin[seg] * seg_skin[seg];
+        st.trig_out = 0.25f * margin * margin;
         st.nsteps = A.seg_steps[seg];
         st.t0 = A.seg_t0[seg];
         st.t1 = A.seg_t1[seg];
@@ -3389,7 +3538,12 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                         hipLaunchKernelGGL(pop_integrate_kernel, grid_of(g), blk, 0, sg, V[g], st);
                         hipLaunchKernelGGL(sort_kern, dim3(ns), dim3(kPopSortNT), sort_lds, sg, V[g], st.fp);
                         hipLaunchKernelGGL(pop_permute_kernel<!kPopFused>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
-                        if (!kPopFused) hipLaunchKernelGGL(pop_fill_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                        if (Q.two) {
+                            hipLaunchKernelGGL(pop_fill_kernel<kOuterRow>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                            hipLaunchKernelGGL(pop_refilter_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                        } else if (!kPopFused) {
+                            hipLaunchKernelGGL(pop_fill_kernel<kPopListRow>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                        }
                         hipLaunchKernelGGL(pop_force_kernel<kPopFused>, grid_of(g), blk, 0, sg, V[g], evf, envf, st);
                     }
                 }
