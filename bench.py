@@ -434,6 +434,8 @@ def main():
     for _ in range(args.steps):
         tm = it.step()
         anneal_ms.append(it.ctx.kernel_ms('anneal'))
+        if os.environ.get('IGM_PROF'):  # tuning: the LDS anneal kernel's cycle profile (perturbs the timing)
+            print('[prof]', json.dumps(it.ctx.mstep_profile()), file=sys.stderr, flush=True)
         bytes_launch.append(it.algorithmic_anneal_bytes())
         astep_s.append(tm['astep_s'])
         mstep_s.append(tm['mstep_s'])

@@ -57,3 +57,14 @@ def test_gpu_two_ranks_equal_one_rank(tmp_path):
         assert float(p['score']) == score
         assert np.array_equal(p['restored'], xyz[s0:s1])  # checkpoint after a step, resumed per rank
     assert len(rows) > 1000 and ptr[-1] > 1000
+
+
+def test_gpu_rccl_collectives_one_rank():
+    """The RCCL ('nccl') path of the collective helpers runs on device tensors (one rank:
+    RCCL refuses two ranks on one GPU; the two-rank equality above runs over gloo)."""
+    env = dict(os.environ, OMP_NUM_THREADS='2')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1',
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'rccl_worker.py')]
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=180)
+    assert r.returncode == 0 and 'RCCL-OK' in r.stdout, r.stdout[-4000:]
+
