@@ -15,7 +15,7 @@ for v in ${VARIANTS:-new old new}; do
     for kv in ${envs//,/ }; do export "$kv"; done
     [ -n "$SKIN" ] && export IGM_SKIN_FACTOR=$SKIN
     IGM_HIP_LIB=$PWD/$lib timeout -k 10 600 python -u bench.py --config ${CONFIG:-B} --nstruct ${NSTRUCT:-1000} \
-      --protocol-scale ${SCALE:-0.2} --steps 1 --warmup 0 --cpu-sample 0 --no-de --no-c > gpurun_out/tune_${CONFIG:-B}_${i}_$tag.log 2>&1
+      --protocol-scale ${SCALE:-0.2} --steps 1 --warmup ${WARMUP:-0} --cpu-sample 0 --no-de --no-c > gpurun_out/tune_${CONFIG:-B}_${i}_$tag.log 2>&1
   )
   rc=$?; echo "$v rc=$rc"; [ $rc -eq 0 ] || exit $rc
   i=$((i+1))
