@@ -1309,6 +1309,7 @@ struct PopArgs {
     int* oflag[2];       // (B) outer margin exceeded, by step parity
     int* flist2;         // (B) the structures whose inner list is rebuilt this step
     int* nflag2;         // (1)
+    unsigned long long* sprof;  // optional (8): the sort kernel's phase cycles, summed (profiling)
 };
 
 // one Verlet list of the engine (the inner one, or the outer one of two-level lists)
@@ -1492,6 +1493,9 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
 // N <= APT * kPopSortNT) in registers, and all their loads are in flight together --
 // the sort is one workgroup's chain of dependent memory round trips, so fewer and
 // wider trips are what makes it faster.
+#ifndef IGM_POP_SORT_PROF
+#define IGM_POP_SORT_PROF 0  // 1: per-phase cycle counters of the sort (with IGM_POP_SORT_PROF set at run time)
+#endif
 template <bool IDS_LDS, int APT>
 __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cw[];  // (kPopCells + 1) / 2 words, then ids
@@ -1500,6 +1504,18 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
     __shared__ int sn[3];
     const int s = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     if (!A.flag[fp][s]) return;
+#if IGM_POP_SORT_PROF
+    unsigned long long tp = A.sprof ? clock64() : 0;
+    auto phase = [&](int k) {  // profiling builds: thread 0 charges the cycles since the last mark
+        if (A.sprof && t == 0) {
+            const unsigned long long now = clock64();
+            atomicAdd(&A.sprof[k], now - tp);
+            tp = now;
+        }
+    };
+#else
+    auto phase = [](int) {};
+#endif
     if (A.two) {  // every rebuild re-filters the inner list; the outer one waits for its margin
         if (t == 0) A.flist2[atomicAdd(A.nflag2, 1)] = s;
         if (!A.oflag[fp][s]) return;
@@ -1557,6 +1573,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
     uint16_t* ids = reinterpret_cast<uint16_t*>(cw + ((kPopCells + 1) >> 1));
     for (int k = t; k < nw; k += kPopSortNT) cw[k] = 0u;
     __syncthreads();
+    phase(0);  // grid from the bbox partials, counts cleared
     constexpr int U = 4;  // independent loads in flight per thread
     uint32_t cr[APT > 0 ? APT : 1];
     if constexpr (APT > 0) {
@@ -1598,6 +1615,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
         }
     }
     __syncthreads();
+    phase(1);  // positions loaded, cells counted
     // exclusive scan of the u16 counts in place (offsets <= N < 65536 fit the halves)
     {
         const int cpt = (nw + kPopSortNT - 1) / kPopSortNT, k0 = t * cpt;
@@ -1620,6 +1638,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
         }
     }
     __syncthreads();
+    phase(2);  // scan
     auto off = [&](int c) -> int { return (int)((cw[c >> 1] >> ((c & 1) << 4)) & 0xffffu); };
     auto put = [&](int k, int v) {
         if (IDS_LDS)
@@ -1657,10 +1676,13 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
             if (i0 + u * kPopSortNT < N) put(off((int)(uu[u] >> 16)) + (int)(uu[u] & 0xffffu), aa[u]);
     }
     __syncthreads();
+    phase(3);  // ids scattered into their cells
     if constexpr (APT > 0) {
         // deterministic order inside a cell: an atom's slot is its cell's first slot plus
         // the number of the cell's atoms with a smaller id (independent LDS reads per
-        // atom, where an insertion sort per cell is a serial chain of them)
+        // atom, where an insertion sort per cell is a serial chain of them).  (Measured,
+        // IGM_POP_SORT_PROF: this phase is ~half of the kernel; keeping slot and id in
+        // registers for coalesced stores after a barrier was 2.5 % slower on the anneal.)
 #pragma unroll
         for (int u = 0; u < APT; ++u) {
             if (t + u * kPopSortNT >= N) continue;
@@ -1691,9 +1713,17 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
             slotn[a] = i;
         }
     }
+    phase(4);  // ranks inside the cells, new slot order stored
     int* cg = A.cell + (size_t)s * kPopCells;
     for (int c = t; c <= ncell + 1; c += kPopSortNT) cg[c] = off(c);
     if (t == 0) A.par[s] = q;
+#if IGM_POP_SORT_PROF
+    if (A.sprof) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (profiling: this wave's stores done)
+        phase(5);  // cell offsets stored
+        if (t == 0) atomicAdd(&A.sprof[6], 1ull);
+    }
+#endif
 }
 
 // LDS bytes of pop_sort_kernel<IDS_LDS>
@@ -3384,6 +3414,13 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.flist = (int*)pfli;
     Q.nflag = (int*)pnf;
     Q.nflag2 = (int*)pnf + 32;
+    const bool sprof = IGM_POP_SORT_PROF && getenv("IGM_POP_SORT_PROF") != nullptr;  // profiling builds only
+    if (sprof) {
+        void* psp;
+        IGM_TRY(workspace(c, "pop_sprof", sizeof(unsigned long long) * 8, &psp));
+        IGM_HIP_CHECK(c, hipMemsetAsync(psp, 0, sizeof(unsigned long long) * 8, c->stream));
+        Q.sprof = (unsigned long long*)psp;
+    }
     Q.kep = (double*)pke;
     Q.bbp = (float*)pbb;
     Q.nrebuild = (int*)pnr;
@@ -3561,6 +3598,14 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     }
     IGM_HIP_CHECK(c, hipGetLastError());
     IGM_TRY(aux_join(c, nc));
+    if (sprof) {
+        unsigned long long v[8];
+        IGM_HIP_CHECK(c, hipMemcpyAsync(v, Q.sprof, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
+        const double n = (double)(v[6] ? v[6] : 1);
+        fprintf(stderr, "[igm pop sort] %llu sorts; cycles per sort: grid %.0f count %.0f scan %.0f scatter %.0f rank %.0f "
+                        "offsets %.0f\n", v[6], v[0] / n, v[1] / n, v[2] / n, v[3] / n, v[4] / n, v[5] / n);
+    }
     return IGM_OK;
 }
 

@@ -627,12 +627,11 @@ __device__ __forceinline__ bool dd_build(const DdArgs& D, int s, float cut_list)
 
 template <int NT, int BPT>
 __global__ void __launch_bounds__(NT) dd_anneal_kernel(DdArgs D) {
-    constexpr int NW = NT / 64;
-    constexpr int kOwnCap = dd_own_cap(NT, BPT), kResCap = dd_res_cap(NT, BPT);
+    constexpr int kOwnCap = dd_own_cap(NT, BPT);
     const AnnealArgs& A = D.A;
     const int N = A.cm.natom;
     DdLds sm = carve_dd_lds(dd_lds, N, NT, BPT);
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int t = threadIdx.x;
     // optional phase profile: thread 0 charges the wall-clock time since the last mark
     const bool prof = D.prof != nullptr;
     long long tmark = prof ? wall_clock64() : 0;
