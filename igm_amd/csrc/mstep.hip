@@ -46,6 +46,10 @@ constexpr int kCellCapBig = 32768;        // cell grid of an HBM-resident struct
 constexpr size_t kLdsBytes = 160 * 1024 - 1024;  // dynamic LDS per workgroup: 160 KB per CU (gfx950) less a static reserve
 constexpr int kNeighBudget = 64;          // default Verlet-list slots per atom
 constexpr int kLdsListSlots = 8;          // LDS path: the first slots of every atom's list live in LDS
+#ifndef IGM_BOND_PRUNE
+#define IGM_BOND_PRUNE 1  // LDS anneal: bonds that cannot act before the next list build are skipped
+#endif
+constexpr bool kBondPrune = IGM_BOND_PRUNE != 0;
 #ifndef IGM_BOND_BATCH
 #define IGM_BOND_BATCH 2  // LDS bonds per batch (config B anneal: 2 is 1.1% faster than 4)
 #endif
@@ -811,6 +815,30 @@ __device__ __forceinline__ float soft_pair_t(float r2, float rc) {
     return r2 > 0.0f ? rc2 * t * s : 0.0f;
 }
 
+// LDS bond entries 0..31 of an atom at p that may act before the next Verlet-list
+// build (bit k: entry k).  Between builds every bead moves at most skin/2 (the
+// `check yes` trigger), so a bead-bead distance changes by less than skin: an upper
+// bound whose build distance is below r0 - skin (a lower bound: above r0 + skin)
+// contributes exactly 0 until then.  Non-bead atoms are not watched by the trigger,
+// so their bonds stay candidates.  1 % of the skin covers the f32 rounding.
+__device__ __forceinline__ uint32_t bond_candidates(const float4& p, const uint16_t* l, int n, const float4* btab,
+                                                    const float4* pos, float skin) {
+    if (!(p.w >= 0.0f)) return 0xffffffffu;
+    const float d = 1.01f * skin;
+    uint32_t m = 0u;
+    const int n32 = n < 32 ? n : 32;
+    for (int k = 0; k < n32; ++k) {
+        const uint32_t ev = l[k];
+        const float4 pj = pos[ev & 0xfffu];
+        const float r0 = __builtin_sqrtf(btab[ev >> 13].x);
+        const float dx = p.x - pj.x, dy = p.y - pj.y, dz = p.z - pj.z;
+        const float r = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
+        const bool idle = pj.w >= 0.0f && (((ev >> 12) & 1u) ? r - d > r0 : r + d < r0);
+        m |= idle ? 0u : 1u << k;
+    }
+    return m;
+}
+
 // f32 MD force of atom a in the LDS anneal kernel.  Pairs in two passes over
 // the Verlet list: a distance filter over every entry (one bit per entry inside
 // r_i + r_j) and the soft-pair force of the flagged entries only.  In a relaxed
@@ -823,7 +851,8 @@ template <int U>
 __device__ __forceinline__ void atom_force_md(int s, int a, const float4& p0, uint32_t fl, const float4* pos,
                                               const NList<float, uint16_t>& L, float bx, float by, float bz,
                                               const BondView& B, const DevParams& P, float evf,
-                                              float envf, float& fx, float& fy, float& fz, int amax) {
+                                              float envf, float& fx, float& fy, float& fz, int amax,
+                                              uint32_t bmask = 0xffffffffu) {
     fx = fy = fz = 0.0f;
     const float xi = p0.x, yi = p0.y, zi = p0.z, ri = p0.w;
     double unused = 0.0;
@@ -891,11 +920,26 @@ __device__ __forceinline__ void atom_force_md(int s, int a, const float4& p0, ui
         }
     }
     if (B.l) {
+        // entries 0..31 whose bit in bmask is clear cannot act before the next list
+        // build (bond_candidates); the rest are visited in entry order as before
         constexpr int UL = IGM_BOND_BATCH;  // LDS bond entries per batch, branch-free
-        for (int k0 = 0; k0 < B.n; k0 += UL) {
+        uint32_t bm = bmask;
+        int kh = 32;
+        for (;;) {
+            int ku[UL];
+#pragma unroll
+            for (int u = 0; u < UL; ++u) {
+                if (bm) {
+                    ku[u] = __builtin_ctz(bm);
+                    bm &= bm - 1u;
+                } else {
+                    ku[u] = kh++;
+                }
+            }
+            if (ku[0] >= B.n) break;
             uint32_t ev[UL];
 #pragma unroll
-            for (int u = 0; u < UL; ++u) ev[u] = (uint32_t)B.l[k0 + u < B.n ? k0 + u : B.n - 1];
+            for (int u = 0; u < UL; ++u) ev[u] = (uint32_t)B.l[ku[u] < B.n ? ku[u] : B.n - 1];
             float4 q[UL];
             float4 pj[UL];
 #pragma unroll
@@ -910,7 +954,7 @@ __device__ __forceinline__ void atom_force_md(int s, int a, const float4& p0, ui
                 // upper bound active beyond r0, lower bound inside it
                 const bool act = (r2 > q[u].x) != (((ev[u] >> 12) & 1u) != 0u);
                 const float fb = q[u].y * __builtin_amdgcn_rsqf(fmaxf(r2, 1.0e-30f)) + q[u].z;
-                const float m = (act && k0 + u < B.n) ? fb : 0.0f;
+                const float m = (act && ku[u] < B.n) ? fb : 0.0f;
                 fx += m * dx;
                 fy += m * dy;
                 fz += m * dz;
@@ -1010,6 +1054,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
     const int t = threadIdx.x, lane = t & 63;
     const int natom = A.cm.natom;
     float v[BPT][3], f[BPT][3], xb[BPT][3];
+    uint32_t bmk[BPT];  // LDS bond entries 0..31 that may act before the next list build
     for (;;) {
         const int s = next_structure(A.cm, sm.r.misc);
         if (s >= A.cm.nstruct) break;
@@ -1037,6 +1082,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                 f[b][d] = 0.0f;
                 xb[b][d] = __int_as_float(0x7f800000);  // +inf: forces the first neighbour build
             }
+            bmk[b] = 0xffffffffu;
         }
         double cnt[1] = {(double)nmob};
         block_sum<NT, 1>(cnt, sm.r.red0);
@@ -1121,10 +1167,15 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                     ++nbuild;
 #pragma unroll
                     for (int b = 0; b < BPT; ++b) {
-                        const float4 p = sm.pos[b * NT + t];
+                        const int a = b * NT + t;
+                        const float4 p = sm.pos[a];
                         xb[b][0] = p.x;
                         xb[b][1] = p.y;
                         xb[b][2] = p.z;
+                        bmk[b] = 0xffffffffu;
+                        if (kBondPrune && lds_bonds && a < natom)
+                            bmk[b] = bond_candidates(p, sm.rest + sm.boff[a], (int)sm.boff[a + 1] - (int)sm.boff[a],
+                                                     sm.btab, sm.pos, skin);
                     }
                 }
                 // forces: the owner thread gathers every contribution of its atoms (one
@@ -1143,7 +1194,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                         atom_force_md<kLdsPairBatch>(s, a, sm.pos[a], fla, sm.pos,
                                                      sm.L, pick<BPT>(xb, b, 0), pick<BPT>(xb, b, 1),
                                                      pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz,
-                                                     natom - 1);
+                                                     natom - 1, pick<BPT>(bmk, b));
 #pragma unroll
                         for (int i = 0; i < BPT; ++i)
                             if (b == i) {
