@@ -1284,7 +1284,15 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
 // reproducible.
 constexpr int kPopBS = 256;
 constexpr int kPopSortNT = 1024;
-constexpr int kPopCells = kCellCapBig + 2;  // cell offsets of a structure: real cells, non-bead run, end
+#ifndef IGM_POP_CELL_CAP
+#define IGM_POP_CELL_CAP 49152
+#endif
+// cells of a structure's grid in the population engine: the sort keeps their u16 counts
+// and the structure's u16 atom ids in one CU's LDS (49 152 cells + 29 838 ids: 158 KB), so
+// the cold runs' short cut_list (0.45 rmax skin: 35^3 cells over a 200 kb nucleus) keeps
+// cells of side cut_list instead of enlarging them past it
+constexpr int kPopCellCap = IGM_POP_CELL_CAP;
+constexpr int kPopCells = kPopCellCap + 2;  // cell offsets of a structure: real cells, non-bead run, end
 #ifndef IGM_POP_FILL_W
 #define IGM_POP_FILL_W 4
 #endif
@@ -1327,6 +1335,7 @@ struct PopArgs {
     uint2* nl;           // (B, nslice, kq, 64) Verlet list: quads of u16 slot ids, padded with the own slot
     uint16_t* nnb;       // (B, ldn) list length, or kNnbWalk
     int* cell;           // (B, kPopCells) first slot of every cell of the build grid
+    int ccap;            // cells per grid of this run (<= kPopCellCap; pop_sort_cells)
     float* gp;           // (B, 8) grid lo[3], inv[3]
     int* gn;             // (B, 8) grid nb[3]
     uint32_t* bent;      // (B, nslice, bdmax, 64) bonds of a slot: partner slot | type << 16 | lower << 31
@@ -1534,7 +1543,7 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
 }
 
 // One workgroup per flagged structure: the cell grid of build_nlist (cells of side >=
-// cut_list, at most kCellCapBig) from the bbox partials, then a counting sort of the
+// cut_list, at most kPopCellCap) from the bbox partials, then a counting sort of the
 // slots into it -- cell counts as packed u16 pairs in LDS, and with IDS_LDS the new
 // order of atom ids too (u16), so the ranks, the scan and the per-cell insertion
 // sort (ascending ids: deterministic) never leave the CU.  Non-bead atoms form a last
@@ -1601,7 +1610,8 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
             vol *= fmaxf(ext[d], cut);
         }
         float cs = cut;
-        if (vol / (cs * cs * cs) > (float)kCellCapBig) cs = cbrtf(vol / (float)kCellCapBig) * 1.0001f;
+        const float cap = (float)A.ccap;
+        if (vol / (cs * cs * cs) > cap) cs = cbrtf(vol / cap) * 1.0001f;
         float* gp = A.gp + (size_t)s * 8;
         int* gn = A.gn + (size_t)s * 8;
 #pragma unroll
@@ -1621,7 +1631,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
     const int nb[3] = {sn[0], sn[1], sn[2]};
     const int ncell = nb[0] * nb[1] * nb[2];
     const int nw = (ncell + 3) >> 1;  // words holding the cells 0..ncell+1
-    uint16_t* ids = reinterpret_cast<uint16_t*>(cw + ((kPopCells + 1) >> 1));
+    uint16_t* ids = reinterpret_cast<uint16_t*>(cw + ((A.ccap + 3) >> 1));
     for (int k = t; k < nw; k += kPopSortNT) cw[k] = 0u;
     __syncthreads();
     phase(0);  // grid from the bbox partials, counts cleared
@@ -1777,10 +1787,20 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
 #endif
 }
 
-// LDS bytes of pop_sort_kernel<IDS_LDS>
-__host__ __device__ inline size_t pop_sort_lds(bool ids_lds, int natom) {
-    return sizeof(uint32_t) * ((kPopCells + 1) / 2) + (ids_lds ? sizeof(uint16_t) * (size_t)natom : 0);
+// LDS bytes of pop_sort_kernel<IDS_LDS> over grids of at most ccap cells
+__host__ __device__ inline size_t pop_sort_lds(bool ids_lds, int natom, int ccap) {
+    return sizeof(uint32_t) * ((ccap + 3) / 2) + (ids_lds ? sizeof(uint16_t) * (size_t)natom : 0);
 }
+
+// the grid cap of a run: kPopCellCap when the ids fit beside its counts in LDS, else the
+// largest cap (>= kCellCapBig) that keeps them there, else kPopCellCap with HBM ids
+inline int pop_sort_cells(int natom) {
+    if (pop_sort_lds(true, natom, kPopCellCap) <= kLdsBytes) return kPopCellCap;
+    const long long room = ((long long)kLdsBytes - 2LL * natom) / 2 - 4;
+    if (room >= kCellCapBig) return (int)(room & ~63LL);
+    return kPopCellCap;
+}
+static_assert(kPopCells < 65536, "cell ids are packed in 16 bits");
 
 // logical block of the build kernels over the compacted flagged structures (plain
 // order: the working blocks are dealt over all XCDs); false for an idle block
@@ -3524,8 +3544,9 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         Q.csr = (const uint32_t*)pcsr;
     }
     // the sort keeps its ids in LDS when they fit beside the cell counts (200 kb: 29 839 atoms)
-    const bool ids_lds = pop_sort_lds(true, N) <= kLdsBytes;
-    const size_t sort_lds = pop_sort_lds(ids_lds, N);
+    Q.ccap = pop_sort_cells(N);
+    const bool ids_lds = pop_sort_lds(true, N, Q.ccap) <= kLdsBytes;
+    const size_t sort_lds = pop_sort_lds(ids_lds, N, Q.ccap);
     auto sort_kern = !ids_lds ? pop_sort_kernel<false, 0>
                      : N <= 16 * kPopSortNT ? pop_sort_kernel<true, 16>
                      : N <= 32 * kPopSortNT ? pop_sort_kernel<true, 32> : pop_sort_kernel<true, 0>;
