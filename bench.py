@@ -13,14 +13,16 @@ rank owns its own block of 1000 structure ids), Hi-C pairs of the demo .hcs at
 sigma = 0.02, the demo annealing protocol (47 000 MD steps + CG), synthetic
 territory initial coordinates (RandomInit semantics, seeded).
 
-config_C block (the metric's own workload, BASELINE configs[2]): 200 kb diploid,
-pop = --c-total structures STRONG-split over the ranks (default 1000 with several
-GPUs: at 8 GPUs the 125-structure shards of pop=1000, the north-star run; 125 on one
-GPU), Hi-C sigma 0.01, full protocol, the A-step over the whole population after one
-RCCL all-gather; c_warmup + c_steps A/M iterations between barriers, max over ranks.
+config_C block (the metric's own workload, BASELINE.json "200kb diploid pop=1000"):
+200 kb diploid, pop = --c-total (default 1000) structures STRONG-split over the ranks
+(all 1000 on one GPU; at 8 GPUs the 125-structure shards, the north-star run), Hi-C
+sigma 0.01, full protocol, the A-step over the whole population after one RCCL
+all-gather; c_warmup + c_steps A/M iterations between barriers, max over ranks.
 CPU baselines (rank 0, N=1): the fp64 C port on the state of the first TIMED step
-(snapshot after the warmup: same coordinates, restraints, seeds), threads = the
-box's CPU share (affinity), at most --cpu-threads.
+(snapshot after the warmup: same coordinates, restraints, seeds), one structure per
+thread on every CPU the process may use (the affinity mask capped by the cgroup CPU
+quota: 16 of the 256 visible CPUs on the GPU box), with the per-core rate and its
+linear extrapolation to every visible CPU.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
 torch.distributed.run (one process per GPU, RCCL).
@@ -48,8 +50,10 @@ def parse():
                     help='B: 2 Mb diploid (the N=1 metric workload); C: 200 kb diploid (29 838 beads)')
     ap.add_argument('--nstruct', type=int, default=None, help='structures per GPU (B: 1000, C: 125)')
     ap.add_argument('--sigma', type=float, default=None, help='Hi-C sigma (B: 0.02, C: 0.01)')
-    ap.add_argument('--cpu-sample', type=int, default=16, help='structures in the CPU baseline sample (0: skip)')
-    ap.add_argument('--cpu-threads', type=int, default=16, help='at most this many host threads (the box\'s share)')
+    ap.add_argument('--cpu-sample', type=int, default=-1,
+                    help='structures in the CPU baseline sample (-1: one per host thread; 0: skip)')
+    ap.add_argument('--cpu-threads', type=int, default=0,
+                    help='at most this many host threads (0: every CPU the affinity mask and cgroup quota grant)')
     ap.add_argument('--no-de', action='store_true', help='skip the configuration D/E A-step measurement')
     ap.add_argument('--sprite-clusters', type=int, default=20000, help='SPRITE clusters in the D/E measurement')
     ap.add_argument('--protocol-scale', type=float, default=1.0,
@@ -57,8 +61,7 @@ def parse():
     ap.add_argument('--no-c', action='store_true', help='skip the config C (200 kb) block of the N=1 line')
     ap.add_argument('--c-steps', type=int, default=1, help='timed A/M iterations of the config C block')
     ap.add_argument('--c-total', type=int, default=None,
-                    help='config C population split over the ranks (default: 1000 with several GPUs -- the '
-                         'metric -- and the 125-structure shard of pop=1000 at 8 GPUs on one)')
+                    help='config C population split over the ranks (default 1000: the metric\'s workload)')
     ap.add_argument('--c-warmup', type=int, default=1, help='warmup A/M iterations of the config C block')
     ap.add_argument('--c-cpu-scale', type=float, default=0.02,
                     help='protocol scale of the config C CPU-baseline sample (0: skip it)')
@@ -68,7 +71,7 @@ def parse():
     if a.sigma is None:
         a.sigma = 0.02 if a.config == 'B' else 0.01
     if a.c_total is None:
-        a.c_total = 1000 if int(os.environ.get('WORLD_SIZE', '1')) > 1 else 125
+        a.c_total = 1000
     return a
 
 
@@ -96,15 +99,49 @@ def build_inputs(args, rank):
     return dict(pop=pop, atoms=atoms, xyz=xyz, chrom=chrom, poly=poly, prm=prm, pairs=pairs, first=first)
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max, v1
+    cfs_quota/period), or None when unlimited.  On the GPU box the affinity mask shows
+    every CPU of the machine (256) but cpu.max grants 16 (scripts/probe_cpu.py:
+    16 threads 30.3 structures/s, 256 threads 20.3 -- oversubscribed)."""
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as fh:
+            q, per = fh.read().split()[:2]
+        return None if q == 'max' else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as fh:
+            q = float(fh.read())
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as fh:
+            per = float(fh.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def host_threads(args):
-    """threads for the CPU baselines: --cpu-threads, at most the CPUs this process may
-    run on (on the GPU box os.cpu_count() shows the whole machine, the box's share is
-    the affinity mask)"""
+    """threads for the CPU baselines: every CPU this process may use -- the affinity
+    mask, capped by the cgroup's CPU quota (more threads than the quota only time-slice
+    the same CPU time) -- and at most --cpu-threads when given.  Returns (threads,
+    affinity CPUs, quota or None)."""
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    return max(1, min(args.cpu_threads, avail)), avail
+    quota = cgroup_cpu_quota()
+    n = avail if quota is None else max(1, min(avail, int(quota)))
+    if args.cpu_threads > 0:
+        n = min(n, args.cpu_threads)
+    return n, avail, quota
+
+
+def host_fields(nth, avail, quota, rate):
+    """the host-CPU fields every CPU baseline carries: threads used, the CPUs visible,
+    the cgroup quota, the per-core rate and its linear extrapolation to every visible
+    CPU (an upper bound for the CPU side: no SMT or memory-bandwidth loss assumed)"""
+    return {'cores': nth, 'host_cpus_visible': avail, 'cgroup_cpu_quota': quota, 'per_core': rate / nth,
+            'all_host_cpus_linear': rate / nth * avail}
 
 
 def step_restraints(it, snap):
@@ -127,10 +164,10 @@ def cpu_baseline(args, it, inp, snap):
     import oracle
     from igm_amd import model as M
     from igm_amd._lib import bond_dtype
-    nth, avail = host_threads(args)
+    nth, avail, quota = host_threads(args)
     ptr, bonds, xall, step_no = step_restraints(it, snap)
     bonds = bonds.view(bond_dtype)
-    n = min(args.cpu_sample, it.S_local)
+    n = min(nth if args.cpu_sample < 0 else args.cpu_sample, it.S_local)
     sptr = ptr[:n + 1].copy()
     sb = bonds[:sptr[-1]].copy()
     x = np.ascontiguousarray(xall[:n])
@@ -139,11 +176,13 @@ def cpu_baseline(args, it, inp, snap):
     oracle.mstep_run(inp['prm'], x, inp['atoms'].radii, inp['atoms'].flags, inp['poly'], sptr, sb, seeds,
                      nthreads=min(nth, n))
     dt = time.perf_counter() - t0
-    return {'value': n / dt, 'unit': 'structures/s', 'cores': min(nth, n), 'host_cpus_visible': avail,
-            'kind': 'port',
-            'sample': '%d structures of config B at the state of the first timed step (after %d warmup A/M '
-                      'iterations: same coordinates, Hi-C restraints and seeds as that GPU step), full demo protocol, '
-                      'fp64 C restatement, one structure per thread, %.1f s' % (n, args.warmup, dt)}
+    out = {'value': n / dt, 'unit': 'structures/s', 'kind': 'port'}
+    out.update(host_fields(min(nth, n), avail, quota, n / dt))
+    out['sample'] = ('%d structures of config B at the state of the first timed step (after %d warmup A/M '
+                     'iterations: same coordinates, Hi-C restraints and seeds as that GPU step), full demo protocol, '
+                     'fp64 C restatement, one structure per thread on %d threads (affinity %d CPUs, cgroup quota %s '
+                     'CPUs), %.1f s' % (n, args.warmup, min(nth, n), avail, quota, dt))
+    return out
 
 
 def cpu_baseline_c(args, it, inp, snap, warmup):
@@ -156,7 +195,7 @@ def cpu_baseline_c(args, it, inp, snap, warmup):
     import oracle
     from igm_amd import model as M
     from igm_amd._lib import bond_dtype
-    nth, avail = host_threads(args)
+    nth, avail, quota = host_threads(args)
     ptr, bonds, xall, step_no = step_restraints(it, snap)
     bonds = bonds.view(bond_dtype)
     n = min(nth, it.S_local)
@@ -178,11 +217,15 @@ def cpu_baseline_c(args, it, inp, snap, warmup):
     oracle.mstep_run(prm, x.copy(), inp['atoms'].radii, inp['atoms'].flags, inp['poly'], sptr, sb, seeds, nthreads=n)
     t_cg = time.perf_counter() - t0
     t_full = max(t_sample - t_cg, 0.0) / sc + t_cg
-    return {'value': n / t_full, 'unit': 'structures/s', 'cores': n, 'host_cpus_visible': avail, 'kind': 'port',
-            'sample': '%d structures of config C at the state of the first timed step (after %d warmup A/M '
-                      'iterations: same coordinates, Hi-C restraints and seeds), fp64 C restatement, one structure '
-                      'per thread; demo protocol MD steps x%g: %.1f s, CG alone %.1f s, extrapolated to the full '
-                      'protocol %.0f s per %d structures' % (n, warmup, sc, t_sample, t_cg, t_full, n)}
+    out = {'value': n / t_full, 'unit': 'structures/s', 'kind': 'port', 'extrapolated': True}
+    out.update(host_fields(n, avail, quota, n / t_full))
+    out['sample'] = ('%d structures of config C at the state of the first timed step (after %d warmup A/M '
+                     'iterations: same coordinates, Hi-C restraints and seeds), fp64 C restatement, one structure '
+                     'per thread on %d threads (affinity %d CPUs, cgroup quota %s CPUs); demo protocol MD steps x%g: '
+                     '%.1f s, CG alone %.1f s, extrapolated to the full protocol %.0f s per %d structures (a '
+                     'full-protocol measurement: profiles/r04_cpu_c/)' % (n, warmup, n, avail, quota, sc, t_sample,
+                                                                          t_cg, t_full, n))
+    return out
 
 
 def syn_protocol():
@@ -206,6 +249,7 @@ def cpu_baseline_astep(args, it, nthreads, npairs=4000):
                    it.hap_chrom.cpu().numpy(), pairs, float(it.cr), int(it.it_corr), nthreads=nthreads)
     dt = time.perf_counter() - t0
     return {'value': len(sub) / dt, 'unit': 'pairs/s', 'cores': nthreads, 'kind': 'port',
+            'per_core': len(sub) / dt / nthreads,
             'sample': '%d seeded pairs of the same list, %d structures, %.2f s' % (len(sub), it.S_total, dt)}
 
 
@@ -427,7 +471,7 @@ def main():
     for _ in range(args.warmup):
         it.step()
     barrier()
-    want_cpu = args.cpu_sample > 0 and world == 1 and rank == 0
+    want_cpu = args.cpu_sample != 0 and world == 1 and rank == 0
     snap = it.snapshot() if want_cpu else None  # the first timed step's input state
     anneal_ms, bytes_launch, astep_s, mstep_s = [], [], [], []
     t0 = time.perf_counter()
@@ -448,8 +492,8 @@ def main():
     nrows, nbonds, S_local, npairs, npairs_total = int(it.nrows), it.nbonds, it.S_local, it.npairs, it.npairs_total
     de = cblock = astep_cpu = cpu = None
     if want_cpu:
-        nth, _ = host_threads(args)
-        astep_cpu = cpu_baseline_astep(args, it, nth)
+        nth, _, _ = host_threads(args)
+        astep_cpu = cpu_baseline_astep(args, it, nth, npairs=2000 * nth)
         cpu = cpu_baseline(args, it, inp, snap)
     if rank == 0 and world == 1 and not args.no_de:  # the N=1 line carries it; scaling runs stay lean
         de = bench_asteps_de(args, it.ctx)

@@ -25,7 +25,6 @@ IGM_ASYNC = 0x2
 IGM_F32_PATH = 0x4
 IGM_MSTEP_FORCE_GLOBAL = 0x1  # igm_mstep_params.flags: HBM-resident kernels even when LDS fits
 IGM_MSTEP_STRUCT_FLAGS = 0x2  # igm_mstep_params.flags: atom_flags is (nstruct, natom)
-IGM_MSTEP_ENGINE_DD = 0x4  # igm_mstep_params.flags: HBM-size structures on the domain-decomposed LDS engine
 
 IGM_MAX_STAGES = 16
 IGM_MAX_ENVELOPES = 4
@@ -109,7 +108,6 @@ SIGNATURES = {
     'igm_ctx_synchronize': (_i32, [_vp]),
     'igm_last_kernel_ms': (_f64, [_vp, ctypes.c_char_p]),
     'igm_mstep_last_profile': (_i32, [_vp, _vp]),
-    'igm_mstep_engine_stats': (_i32, [_vp, _vp]),
     'igm_version': (ctypes.c_char_p, []),
     'igm_astep_actdist': (_i32, [_vp, _u32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _f64, _i32,
                                  _vp, _vp, _i64, ctypes.POINTER(_i64)]),
@@ -207,12 +205,6 @@ class Context(object):
         self.check(self.lib.igm_mstep_last_profile(self.h, out), 'igm_mstep_last_profile')
         return dict(zip(('build_cycles', 'force_cycles', 'rest_cycles', 'evaluations', 'builds', 'walk_cycles'),
                         list(out)))
-
-    def engine_stats(self):
-        """which engine ran the last anneal of HBM-size structures (igm_mstep_engine_stats)"""
-        out = (ctypes.c_longlong * 8)()
-        self.check(self.lib.igm_mstep_engine_stats(self.h, out), 'igm_mstep_engine_stats')
-        return dict(zip(('domains', 'slots', 'builds', 'recuts', 'max_resident', 'max_owned', 'abort'), list(out)))
 
     def close(self):
         if getattr(self, 'h', None):

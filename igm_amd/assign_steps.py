@@ -25,6 +25,12 @@ from .steps import (Step, PopulationStore, _kernel, _h5_tree, _write_h5, cget, c
                     make_absolute_path, read_damid_rows, rget, sprite_assignment_path)
 
 
+def _rng(seed, k):
+    """the RandomState of batch k of a section seeded `seed` (wrapped to a valid 32-bit
+    seed, so any configured seed works)"""
+    return np.random.RandomState((int(seed) * 1000003 + int(k)) % 2**32)
+
+
 def _rotate(last, current, suffix):
     """the previous result file is kept as '<file>.<suffix...>' (the reduce()s' swapfile)"""
     if last is not None and os.path.isfile(last):
@@ -285,7 +291,7 @@ class SpriteAssignmentStep(Step):
         indptr, data = self._clusters()
         clusters = [data[indptr[c]:indptr[c + 1]] for c in range(batch['c0'], batch['c1'])]
         kb = int(rget(self.cfg, 'restraints/sprite/keep_best', 50))
-        rng = np.random.RandomState(int(cget(self.cfg, 'restraints/sprite/seed', 0)) * 1000003 + batch['batch'])
+        rng = _rng(cget(self.cfg, 'restraints/sprite/seed', 0), batch['batch'])
         idx, val, sel = _kernel(self.cfg, 'sprite')(store, clusters, kb,
                                                     int(rget(self.cfg, 'restraints/sprite/max_chrom_in_cluster', 6)),
                                                     rng, device)
@@ -314,7 +320,7 @@ class SpriteAssignmentStep(Step):
                 val.append(r['val'][q])
                 sel.append(r['sel'][o:o + kb * n].reshape(kb, n))
                 o += kb * n
-        rng = np.random.RandomState(int(cget(self.cfg, 'restraints/sprite/seed', 0)) * 1000003 + 999983)
+        rng = _rng(cget(self.cfg, 'restraints/sprite/seed', 0), 999983)
         rbs = int(cget(self.cfg, 'restraints/sprite/batch_size', 10))  # SpriteAssignmentStep.py:71,171
         nb = -(-self.n_clusters // rbs)
         order = [c for b in rng.permutation(nb) for c in range(b * rbs, min((b + 1) * rbs, self.n_clusters))]
@@ -353,7 +359,7 @@ class PolymerAssignmentStep(Step):
     def task(self, batch, device):
         store = PopulationStore(self.cfg['optimization']['structure_output'])
         d = _h5_tree(self.cfg['restraints']['polymer']['polymer_file'])
-        rng = np.random.RandomState(int(cget(self.cfg, 'restraints/polymer/seed', 0)) * 1000003 + batch['batch'])
+        rng = _rng(cget(self.cfg, 'restraints/polymer/seed', 0), batch['batch'])
         nn = _kernel(self.cfg, 'polymer')(store, np.asarray(batch['loci'], np.int32), d['bin_edges'],
                                           d['probability'], rng, device)
         tmp = batch['out'] + '.part.npy'

@@ -27,7 +27,6 @@ struct igm_ctx {
     // last HBM-size anneal: {K, slots, builds, re-cuts, largest resident set, largest
     // owned set, abort (0: the domain-decomposed engine ran; -1 / > 0: the population
     // engine ran, by choice / after an abort)}
-    long long dd_stats[8] = {0, 0, 0, 0, 0, 0, -1, 0};
     size_t lds_per_block = 65536;
     // auxiliary streams (+ one event each) for independent work inside one call,
     // created on first use: the population engine runs its structure groups on them

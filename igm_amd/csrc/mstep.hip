@@ -1284,6 +1284,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
 // reproducible.
 constexpr int kPopBS = 256;
 constexpr int kPopSortNT = 1024;
+constexpr int kPopMaxGroups = 64;  // structure groups (streams) of one run: build counters nflag[g], nflag2[g]
 #ifndef IGM_POP_CELL_CAP
 #define IGM_POP_CELL_CAP 49152
 #endif
@@ -1413,7 +1414,7 @@ __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float
     if (s >= A.cm.nstruct) return;
     if (lb == 0 && threadIdx.x == 0) {
         *A.nflag = 0;
-        *A.nflag2 = 0;
+        if (A.two) *A.nflag2 = 0;
     }
     if (a == 0) {
         A.flag[0][s] = 1;  // the first step builds
@@ -2298,7 +2299,7 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
     if (s >= A.cm.nstruct) return;
     if (lb == 0 && threadIdx.x == 0) {  // the build kernels of this step are done
         *A.nflag = 0;
-        *A.nflag2 = 0;
+        if (A.two) *A.nflag2 = 0;
     }
     const int rebuilt = A.flag[S.fp][s];  // the structure's list is (was) rebuilt this step
     if (i == 0) {
@@ -2400,7 +2401,6 @@ __global__ void deg_max_kernel(const int* deg, size_t n, int* out) {
     if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
 
-#include "mstep_dd.h"
 
 // 'velocity nonfixed create T seed' (dist uniform, loop all, mom yes) for every
 // structure and segment: RanPark draws in atom-id order, momentum zeroed, scaled
@@ -3381,8 +3381,8 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     V.oflag[1] = Q.oflag[1] + s0;
     V.flist = Q.flist + s0;
     V.flist2 = Q.flist2 + s0;
-    V.nflag = Q.nflag + g;
-    V.nflag2 = Q.nflag + 32 + g;
+    V.nflag = Q.nflag + g;  // one build counter per group, each on its own stream
+    V.nflag2 = Q.nflag2 + g;
     if (Q.two) {
         V.xo = Q.xo + o;
         V.nlo = Q.nlo + (size_t)s0 * nsl * Q.kqo * 64;
@@ -3441,7 +3441,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     IGM_TRY(workspace(c, "pop_bdeg", sizeof(uint16_t) * SL, &pbdeg));
     IGM_TRY(workspace(c, "pop_flag", sizeof(int) * 2 * (size_t)S, &pfl));
     IGM_TRY(workspace(c, "pop_flist", sizeof(int) * (size_t)S, &pfli));
-    IGM_TRY(workspace(c, "pop_nflag", sizeof(int) * 64, &pnf));
+    IGM_TRY(workspace(c, "pop_nflag", sizeof(int) * 2 * kPopMaxGroups, &pnf));
     IGM_TRY(workspace(c, "pop_ke", sizeof(double) * (size_t)S * Q.nbs, &pke));
     IGM_TRY(workspace(c, "pop_bb", sizeof(float) * 6 * (size_t)S * Q.nbs, &pbb));
     void* pnr = A.nrebuild;
@@ -3484,7 +3484,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.flag[1] = (int*)pfl + S;
     Q.flist = (int*)pfli;
     Q.nflag = (int*)pnf;
-    Q.nflag2 = (int*)pnf + 32;
+    Q.nflag2 = (int*)pnf + kPopMaxGroups;
     const bool sprof = IGM_POP_SORT_PROF && getenv("IGM_POP_SORT_PROF") != nullptr;  // profiling builds only
     if (sprof) {
         void* psp;
@@ -3562,7 +3562,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         return e ? atoi(e) : dflt;
     };
     int ng = knob("IGM_POP_GROUPS", 2), nc = knob("IGM_POP_CONC", 0), chunk = knob("IGM_POP_CHUNK", 0);
-    ng = ng < 1 ? 1 : (ng > S ? S : (ng > 64 ? 64 : ng));
+    ng = ng < 1 ? 1 : (ng > S ? S : (ng > kPopMaxGroups ? kPopMaxGroups : ng));
     nc = nc < 1 || nc > ng ? ng : nc;
     if (chunk <= 0) nc = ng;
     IGM_TRY(aux_streams(c, ng));
@@ -3681,180 +3681,11 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     return IGM_OK;
 }
 
-// The domain-decomposed engine (mstep_dd.h) for a batch of structures too large for
-// one CU's LDS.  Sets *fell when it does not apply (LDS layout, occupancy) or when the
-// launch aborted (a domain past its capacity, a barrier past its time limit): the
-// caller then runs the multi-kernel population engine on the restored inputs.
-int run_anneal_dd(igm_ctx* c, const Prepared& pr, const AnnealArgs& A, int kmin_retry, bool* fell) {
-    *fell = true;
-    const int S = pr.cm.nstruct, N = pr.cm.natom;
-    if (A.nseg == 0) return IGM_OK;
-    const int cus = c->num_cus;
-    // Shape: BPT atoms per thread (2 or 3) and K domains per structure, every domain
-    // within 93 % of its owned capacity and its expected resident set within the
-    // resident capacity (measured halo shares on annealed 200 kb structures: 43 % of the
-    // owned atoms at K = 12, 59 % at 16, 75 % at 24; the largest domain's resident set
-    // ~1.35x the mean).  Modelled time: rounds of slots x rounds of 1024 owned atoms per
-    // step x a halo term growing with K.  29 838 atoms, 125 structures: BPT 2, K 16
-    // (8 rounds x 2).
-    int K = 0, bpt = 0, nt = 1024;
-    int want_k = 0, want_b = 0;
-    if (const char* e = getenv("IGM_DD_K")) want_k = atoi(e);
-    if (kmin_retry > 0) want_k = std::min(kmin_retry, std::min(kDdMaxK, cus));
-    if (const char* e = getenv("IGM_DD_BPT")) want_b = atoi(e);
-    if (const char* e = getenv("IGM_DD_NT")) nt = atoi(e) == 768 ? 768 : 1024;
-    double best = 1e300;
-    for (int k = 1; k <= kDdMaxK && k <= cus; ++k) {
-        if (want_k && k != want_k) continue;
-        // the smallest shape that holds the domain (fewer atoms per thread leave the most
-        // LDS for the halo)
-        const int64_t need = ceil_div(N, k);
-        int b = 0;
-        for (int bb = 2; bb <= 4 && !b; ++bb)
-            if ((nt == 1024 ? bb <= 3 : bb >= 3) && need <= (int64_t)(0.93 * dd_own_cap(nt, bb))) b = bb;
-        if (want_b) b = need <= dd_own_cap(nt, want_b) ? want_b : 0;
-        if (b == 0 || !dd_lds_ok(N, nt, b)) continue;
-        // resident set: owned x (1 + halo share), the largest domain ~1.4x the mean
-        if (!want_k && (k > 24 || 1.4 * (double)need * (1.0 + 0.037 * k) > dd_res_cap(nt, b))) continue;
-        const int slots = std::min(cus / k, S);
-        if (slots < 1) break;
-        const double cost = (double)ceil_div(S, slots) * (double)ceil_div(need, nt) * (1.0 + 0.02 * k);
-        if (cost < best) {
-            best = cost;
-            K = k;
-            bpt = b;
-        }
-    }
-    if (K < 1 || bpt < 2 || ceil_div(N, K) > dd_own_cap(nt, bpt)) return IGM_OK;
-    auto kern = nt == 768 ? (bpt == 3 ? dd_anneal_kernel<768, 3> : dd_anneal_kernel<768, 4>)
-                          : (bpt == 2 ? dd_anneal_kernel<1024, 2> : dd_anneal_kernel<1024, 3>);
-    if (nt == 768 && bpt != 3 && bpt != 4) return IGM_OK;
-    const DdLds lay = carve_dd_lds(nullptr, N, nt, bpt);
-    const size_t lds = lay.bytes;
-    IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int per_cu = 0;
-    IGM_HIP_CHECK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, nt, lds));
-    if (per_cu < 1) return IGM_OK;
-    const int nslot = std::min(cus / K, S);
-    const int grid = nslot * K;
-    // the largest bond degree sizes the owned atoms' bond slots
-    void* pdm;
-    IGM_TRY(workspace(c, "dd_dmax", sizeof(int), &pdm));
-    IGM_HIP_CHECK(c, hipMemsetAsync(pdm, 0, sizeof(int), c->stream));
-    hipLaunchKernelGGL(deg_max_kernel, dim3(1024), dim3(256), 0, c->stream, pr.cm.bonds.deg, (size_t)S * N, (int*)pdm);
-    int dmax = 0;
-    IGM_HIP_CHECK(c, hipMemcpyAsync(&dmax, pdm, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
-    DdArgs D;
-    memset(&D, 0, sizeof(D));
-    D.A = A;
-    D.K = K;
-    D.nslot = nslot;
-    D.bdmax = dmax > 0 ? dmax : 1;
-    D.kg = std::max(pr.cm.kcap - kLdsListSlots, 4);
-    D.gstride = ((size_t)dd_own_cap(nt, bpt) * D.kg * 2 + 64 * 2 * IGM_PAIR_BATCH + 255) & ~size_t(255);
-    const char* te = getenv("IGM_DD_TOL");
-    D.tol = te ? (float)atof(te) : 0.08f;
-    int wc_khz = 0;
-    IGM_HIP_CHECK(c, hipDeviceGetAttribute(&wc_khz, hipDeviceAttributeWallClockRate, c->device));
-    D.tmo = (long long)(wc_khz > 0 ? wc_khz : 100000) * 1000LL * 5;  // 5 s per barrier
-    void *px, *pv, *pk, *pvo, *psy, *pbe, *pge, *pst;
-    IGM_TRY(workspace(c, "dd_x", sizeof(float4) * (size_t)nslot * N, &px));
-    IGM_TRY(workspace(c, "dd_v", sizeof(float4) * (size_t)nslot * N, &pv));
-    IGM_TRY(workspace(c, "dd_ke", sizeof(unsigned long long) * (size_t)nslot * kDdMaxK, &pk));
-    IGM_TRY(workspace(c, "dd_vote", sizeof(int) * (size_t)nslot * kDdMaxK, &pvo));
-    const size_t sync_words = (size_t)(nslot + 1) * kDdSyncWords;  // slot counters, then the abort word
-    IGM_TRY(workspace(c, "dd_sync", sizeof(unsigned) * sync_words, &psy));
-    IGM_TRY(workspace(c, "dd_bell", sizeof(uint32_t) * (size_t)grid * dd_own_cap(nt, bpt) * D.bdmax, &pbe));
-    IGM_TRY(workspace(c, "dd_gell", D.gstride * (size_t)grid, &pge));
-    IGM_TRY(workspace(c, "dd_stats", sizeof(unsigned long long) * (8 + kDdProf), &pst));
-    D.X = (float4*)px;
-    D.V = (float4*)pv;
-    D.ke = (unsigned long long*)pk;
-    D.vote = (int*)pvo;
-    D.sync = (unsigned*)psy;
-    D.abort = (int*)((unsigned*)psy + (size_t)nslot * kDdSyncWords);
-    D.bell = (uint32_t*)pbe;
-    D.gell = (unsigned char*)pge;
-    D.stats = (unsigned long long*)pst;
-    const bool dprof = getenv("IGM_DD_PROF") != nullptr;
-    D.prof = dprof ? (unsigned long long*)pst + 8 : nullptr;
-    IGM_HIP_CHECK(c, hipMemsetAsync(psy, 0, sizeof(unsigned) * sync_words, c->stream));
-    IGM_HIP_CHECK(c, hipMemsetAsync(pst, 0, sizeof(unsigned long long) * (8 + kDdProf), c->stream));
-    // inputs kept for a fallback run
-    const size_t n3 = (size_t)S * N * 3;
-    void *px0, *pv0 = nullptr;
-    IGM_TRY(workspace(c, "dd_x0", sizeof(float) * n3, &px0));
-    IGM_HIP_CHECK(c, hipMemcpyAsync(px0, A.xyz, sizeof(float) * n3, hipMemcpyDeviceToDevice, c->stream));
-    if (A.mode == 1) {
-        IGM_TRY(workspace(c, "dd_v0", sizeof(float) * n3, &pv0));
-        IGM_HIP_CHECK(c, hipMemcpyAsync(pv0, A.vel, sizeof(float) * n3, hipMemcpyDeviceToDevice, c->stream));
-    }
-    {
-        Timed tm(c, "anneal");
-        void* args[] = {&D};
-        const hipError_t e =
-            hipLaunchCooperativeKernel((const void*)kern, dim3(grid), dim3(nt), args, (unsigned)lds, c->stream);
-        if (e == hipErrorCooperativeLaunchTooLarge) {
-            (void)hipGetLastError();
-            return IGM_OK;
-        }
-        IGM_HIP_CHECK(c, e);
-    }
-    int ab = 0;
-    unsigned long long st[8 + kDdProf];
-    IGM_HIP_CHECK(c, hipMemcpyAsync(&ab, D.abort, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    IGM_HIP_CHECK(c, hipMemcpyAsync(st, pst, sizeof(st), hipMemcpyDeviceToHost, c->stream));
-    IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
-    c->dd_stats[0] = K;
-    c->dd_stats[1] = nslot;
-    for (int k = 0; k < 4; ++k) c->dd_stats[2 + k] = (long long)st[k];
-    c->dd_stats[6] = ab;
-    if (getenv("IGM_DD_VERBOSE"))
-        fprintf(stderr,
-                "[igm dd] NT=%d BPT=%d K=%d slots=%d builds=%llu recuts=%llu max_res=%llu max_own=%llu max_geo=%llu "
-                "mean_res=%.0f mean_own=%.0f mean_geo=%.0f abort=%d\n",
-                nt, bpt, K, nslot, st[0], st[1], st[2], st[3], st[4], st[5] / (double)std::max(st[0], 1ull),
-                st[6] / (double)std::max(st[0], 1ull), st[7] / (double)std::max(st[0], 1ull), ab);
-    if (dprof) {  // per-workgroup mean, microseconds (wall clock)
-        const double us = 1e3 / (double)(wc_khz > 0 ? wc_khz : 100000), nw = (double)grid;
-        const char* nm[12] = {"integrate", "barA", "handover", "scan", "recut", "bonds", "list", "halo", "force",
-                              "barB", "steps", "builds"};
-        fprintf(stderr, "[igm dd prof] per workgroup:");
-        for (int k = 0; k < 12; ++k)
-            fprintf(stderr, " %s=%.1f%s", nm[k], st[8 + k] * (k < 10 ? us : 1.0) / nw, k < 10 ? "us" : "");
-        fprintf(stderr, "\n");
-    }
-    if (ab) {  // restore the inputs: the caller reruns the batch
-        IGM_HIP_CHECK(c, hipMemcpyAsync(A.xyz, px0, sizeof(float) * n3, hipMemcpyDeviceToDevice, c->stream));
-        if (A.mode == 1)
-            IGM_HIP_CHECK(c, hipMemcpyAsync(A.vel, pv0, sizeof(float) * n3, hipMemcpyDeviceToDevice, c->stream));
-        return IGM_OK;
-    }
-    *fell = false;
-    return IGM_OK;
-}
-
-// HBM-size structures: the multi-kernel population engine, or with params flag
-// IGM_MSTEP_ENGINE_DD (tuning: IGM_POP_ENGINE=dd) the domain-decomposed engine, which
-// falls back to the former when it does not apply or aborts.  (Measured on config C,
-// full demo protocol, 125 structures: population engine 16.1 s, domain-decomposed
-// 31.3 s -- DESIGN.md section 7.)
+// HBM-size structures: the multi-kernel population engine.  (The domain-decomposed
+// engine of round 3 -- 31.3 s against 16.1 s on config C, DESIGN.md section 7 -- is
+// retired; its params flag 0x4 is rejected.)
 int run_anneal_big(igm_ctx* c, const Prepared& pr, const AnnealArgs& A, int32_t pflags) {
-    const char* e = getenv("IGM_POP_ENGINE");
-    const bool dd = (pflags & IGM_MSTEP_ENGINE_DD) || (e && !strcmp(e, "dd"));
-    c->dd_stats[6] = -1;
-    if (dd) {
-        bool fell = true;
-        IGM_TRY(run_anneal_dd(c, pr, A, 0, &fell));
-        if (!fell) return IGM_OK;
-        // a domain past its resident capacity (frustrated structures hold more halo):
-        // once more with more, smaller domains
-        if (c->dd_stats[6] == 1 && c->dd_stats[0] > 0 && c->dd_stats[0] < kDdMaxK) {
-            IGM_TRY(run_anneal_dd(c, pr, A, (int)std::min<long long>(kDdMaxK, c->dd_stats[0] + 8), &fell));
-            if (!fell) return IGM_OK;
-        }
-    }
+    if (pflags & 0x4) return fail(c, IGM_E_UNSUPPORTED, "the domain-decomposed engine (flag 0x4) is retired");
     return run_anneal_pop(c, pr, A);
 }
 
@@ -3935,9 +3766,11 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
     // where atoms move fast (T0 = 5000: 1.0 rmax) and shorter where they barely move
     // (T0 <= 1: 0.45 rmax) -- measured on the demo protocol: config B anneal -2.4 %,
     // config C -1.4 % against one 0.7 rmax skin for every run (scripts/gpu_skin_b.sh,
-    // gpu_skin_seg.sh).  An explicit params.skin is used for every run.
+    // gpu_skin_seg.sh).  An explicit params.skin, or the IGM_SKIN_FACTOR tuning knob (one
+    // skin for every run), is used for every run.
+    const bool uniform_skin = prm->skin > 0 || getenv("IGM_SKIN_FACTOR") != nullptr;
     for (int k = 0; k < A.nseg; ++k) {
-        if (prm->skin > 0) {
+        if (uniform_skin) {
             A.seg_skin[k] = pr.P.skin;
         } else {
             const float rmax = 0.5f * (pr.P.cut_list - pr.P.skin);
@@ -4201,8 +4034,3 @@ extern "C" int igm_mstep_last_profile(igm_ctx* c, unsigned long long* out) {
     return IGM_OK;
 }
 
-extern "C" int igm_mstep_engine_stats(igm_ctx* c, long long* out) {
-    if (!c || !out) return IGM_E_INVALID;
-    for (int k = 0; k < 8; ++k) out[k] = c->dd_stats[k];
-    return IGM_OK;
-}

@@ -40,7 +40,7 @@ class RandomInit(Step):
         seed = int(cget(self.cfg, 'model/init_seed', 0))
         crd = store.coordinates('r+')
         for sid in batch['sids']:
-            rng = np.random.RandomState(seed * 1000003 + sid)
+            rng = np.random.RandomState((seed * 1000003 + sid) % 2**32)  # (a valid RandomState seed for any init_seed)
             crd[:, sid, :] = init.generate_territories(store.chrom_sizes, R, rng).astype(np.float32)
         crd.flush()
         del crd

@@ -35,6 +35,34 @@ def shard(n, rank, world):
     return n * rank // world, n * (rank + 1) // world
 
 
+def pair_combos(pairs, copy_ptr, hap_chrom):
+    """Distance combinations get_actdist evaluates per pair (ActivationDistanceStep.py:
+    405-436): min(|ii|, |jj|) for an intra-chromosome pair (copies zipped), |ii|.|jj|
+    for an inter pair (every combination) -- each one an (S,)-column distance and a
+    row of output."""
+    cp = np.asarray(copy_ptr, np.int64)
+    nc = np.diff(cp)
+    hc = np.asarray(hap_chrom)
+    i, j = np.asarray(pairs['i'], np.int64), np.asarray(pairs['j'], np.int64)
+    ni, nj = nc[i], nc[j]
+    return np.where(hc[i] == hc[j], np.minimum(ni, nj), ni * nj).astype(np.int64)
+
+
+def shard_weighted(weights, rank, world):
+    """Contiguous block [lo, hi) of the units whose weights sum to this rank's equal
+    share (A-step pairs balanced by distance combinations -- an inter
+    pair of two diploid loci costs 4, an intra pair 2).  Contiguous, so the rows in
+    rank order are still the CSR order of one rank."""
+    w = np.asarray(weights, np.int64)
+    if len(w) == 0:
+        return 0, 0
+    cum = np.concatenate([[0], np.cumsum(w)])
+    tot = int(cum[-1])
+    lo = int(np.searchsorted(cum, tot * rank // world, side='left')) if rank > 0 else 0
+    hi = int(np.searchsorted(cum, tot * (rank + 1) // world, side='left')) if rank + 1 < world else len(w)
+    return lo, hi
+
+
 def _staged(t, group):
     """gloo moves host tensors only: device tensors go through host memory (the
     functional multi-process path on one GPU and the CPU tests); RCCL ('nccl') keeps
@@ -57,27 +85,29 @@ def gather_population(xyz_local, group=None):
     return out.to(xyz_local.device) if host else out
 
 
-def gather_rows(rows_u8, nrows, itemsize, group=None):
+def gather_rows(rows_u8, nrows, itemsize, cap, group=None):
     """Concatenate the ranks' A-step rows in rank order, i.e. in CSR pair order
     (task() appends pair after pair, ActivationDistanceStep.py:228-230): the result
-    is byte-identical to one rank processing every pair."""
+    is byte-identical to one rank processing every pair.  `cap` = the largest row
+    count any rank can emit (every rank knows every shard), so one all-gather of
+    fixed-size buffers carries the rows and, in each buffer's last 8 bytes, the
+    count; the host reads the counts once (one sync) to compact."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     host = _staged(rows_u8, group)
     dev = rows_u8.device
     cdev = torch.device('cpu') if host else dev
-    counts = torch.tensor([int(nrows)], dtype=torch.int64, device=cdev)
-    allc = [torch.zeros_like(counts) for _ in range(world)]
-    dist.all_gather(allc, counts, group=group)
-    allc = [int(x.item()) for x in allc]
-    mx = max(max(allc), 1)
-    buf = torch.zeros(mx * itemsize, dtype=torch.uint8, device=cdev)
+    cap = max(int(cap), 1)
+    buf = torch.zeros(cap * itemsize + 8, dtype=torch.uint8, device=cdev)
     buf[:nrows * itemsize] = rows_u8[:nrows * itemsize].to(cdev)
-    bufs = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(bufs, buf, group=group)
-    out = torch.cat([b[:c * itemsize] for b, c in zip(bufs, allc)])
-    return (out.to(dev) if host else out), sum(allc)
+    buf[cap * itemsize:].view(torch.int64).fill_(int(nrows))
+    out = torch.empty(world * buf.numel(), dtype=torch.uint8, device=cdev)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    out = out.view(world, -1)
+    allc = out[:, cap * itemsize:].contiguous().view(torch.int64).view(-1).tolist()  # the one host sync
+    rows = torch.cat([out[r, :c * itemsize] for r, c in enumerate(allc)])
+    return (rows.to(dev) if host else rows), sum(allc)
 
 
 def reduce_sum_f64(values, device, group=None):
@@ -121,9 +151,14 @@ class AMIteration(object):
         self.copy_ptr = T(np.asarray(copy_ptr, np.int32))
         self.copy_idx = T(np.asarray(copy_idx, np.int32))
         self.hap_chrom = T(np.asarray(chrom, np.int32)[:len(copy_ptr) - 1])
-        # contiguous pair shard of this rank (CSR order is kept across ranks)
+        # contiguous pair shard of this rank (CSR order is kept across ranks), balanced
+        # by distance combinations; every rank knows every shard (the row capacity)
         P = len(pairs)
-        self.pair_lo, self.pair_hi = shard(P, rank, world)
+        combos = pair_combos(pairs, copy_ptr, np.asarray(chrom, np.int32)[:len(copy_ptr) - 1])
+        spans = [shard_weighted(combos, r, world) for r in range(world)]
+        self.pair_lo, self.pair_hi = spans[rank]
+        self.row_cap = max(int(combos[lo:hi].sum()) for lo, hi in spans)
+        self._combos = combos
         self.npairs_total = P
         self.pairs = T(np.ascontiguousarray(pairs[self.pair_lo:self.pair_hi], pair_dtype).view(np.uint8))
         self.npairs = self.pair_hi - self.pair_lo
@@ -182,7 +217,7 @@ class AMIteration(object):
                        P(self.per_pair), P(rows), cap, ctypes.byref(n))
         nrows = n.value
         if self.world > 1:
-            rows, nrows = gather_rows(rows, nrows, row_dtype.itemsize, self.group)
+            rows, nrows = gather_rows(rows, nrows, row_dtype.itemsize, self.row_cap, self.group)
         self.rows, self.nrows = rows, nrows
         if self.it_corr == 1 and self.npairs > 0:  # plast of the next iteration (same sigma)
             self._call('igm_astep_update_plast', IGM_DEVICE_PTRS, P(self.pairs), self.npairs, P(self.per_pair))
@@ -258,7 +293,8 @@ class AMIteration(object):
                    P(self.pop_bm), 1)
         pairs_u8 = self.pairs[:self.npairs * pair_dtype.itemsize]
         if self.world > 1:
-            pairs_u8, np_tot = gather_rows(pairs_u8, self.npairs, pair_dtype.itemsize, self.group)
+            cap = max(hi - lo for lo, hi in (shard_weighted(self._combos, r, self.world) for r in range(self.world)))
+            pairs_u8, np_tot = gather_rows(pairs_u8, self.npairs, pair_dtype.itemsize, cap, self.group)
             pairs_u8 = pairs_u8[:np_tot * pair_dtype.itemsize]
         # the score is a collective (all_reduce over the ranks): every rank computes it
         # before the non-writers leave

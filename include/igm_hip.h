@@ -295,9 +295,8 @@ typedef struct {
 #define IGM_MSTEP_STRUCT_FLAGS 0x2 /* atom_flags is (nstruct, natom): per-structure envelope membership
                                       (DamID) and active/inactive centroid slots (SPRITE); the
                                       IGM_ATOM_BEAD bit must be the same in every structure */
-#define IGM_MSTEP_ENGINE_DD 0x4    /* HBM-size structures: the domain-decomposed LDS engine instead of the
-                                      multi-kernel population engine (the default; measured faster on
-                                      the 200 kb model) */
+/* 0x4 is retired (round 3's domain-decomposed engine, 2x slower than the population engine on
+   the 200 kb model): igm_mstep_run returns IGM_E_UNSUPPORTED for it */
 
 /* atom flags (per atom, shared by all structures of a batch) */
 #define IGM_ATOM_BEAD 0x1u   /* takes part in the soft pair potential       */
@@ -370,14 +369,6 @@ int igm_velocity_create(igm_ctx* ctx, uint32_t flags, int32_t nseed, int32_t nat
  * force evaluations, builds, list-fill walks (part of the builds)} summed over the
  * structures of the last launch. */
 int igm_mstep_last_profile(igm_ctx* ctx, unsigned long long* out);
-
-/* Which engine ran the last anneal of HBM-size structures (no reference counterpart:
- * an operational aid for tests and benchmarks).  out[8] = {domains per structure K,
- * structures in flight, list builds, domain re-cuts, largest resident set, largest owned
- * set, abort (0: the domain-decomposed engine ran; -1: the population engine was chosen;
- * > 0: the domain-decomposed launch aborted -- a domain past its capacity or a barrier
- * past its time limit -- and the population engine reran the batch), 0}. */
-int igm_mstep_engine_stats(igm_ctx* ctx, long long* out);
 
 /* ---- M-step restraint assembly: Hi-C contact selection ---------------------
  * interHiC/intraHiC._apply (restraints/inter_hic.py:294-312, intra_hic.py) for

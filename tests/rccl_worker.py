@@ -21,7 +21,7 @@ xyz = torch.randn(7, 3009, 3, generator=g).to(dev)
 out = P.gather_population(xyz)
 assert out.is_cuda and torch.equal(out, xyz)
 rows = torch.randint(0, 255, (16 * 1000,), dtype=torch.uint8, generator=g).to(dev)
-got, n = P.gather_rows(rows, 900, 16)
+got, n = P.gather_rows(rows, 900, 16, 1000)
 assert got.is_cuda and n == 900 and torch.equal(got, rows[:900 * 16])
 vals = [1.5, -2.25, 1e-3]
 red = P.reduce_sum_f64(vals, dev)

@@ -50,7 +50,6 @@ def _run(config):
     seeds = M.lammps_seeds(6535, 700 + sids, 3)
     try:
         xg, ig, sg = A.run(b, seeds, 0.05, ctx)
-        assert ctx.engine_stats()['abort'] == -1  # the population engine ran
         xg2, ig2, _ = A.run(b, seeds, 0.05, ctx)
         if vol is not None:
             oracle.set_volume(vol)

@@ -1,4 +1,4 @@
-"""The N>1 data path of igm_amd.pipeline on CPU (gloo, world_size 2): structure
+"""The N>1 data path of igm_amd.pipeline on CPU (gloo, world_size 2 and 4): structure
 shards -> population all-gather -> pair-sharded A-step -> rows gathered in CSR
 order must equal one rank doing everything.  The per-shard A-step
 compute here is the CPU oracle standing in for the HIP kernel (which the gpu
@@ -31,7 +31,7 @@ def _inputs():
     hic = np.load(os.path.join(GOLDEN, 'demo_hic_pairs.npz'))
     keep = np.where(hic['p'] >= 0.05)[0][:3001]
     pairs = make_pairs(hic['i'][keep], hic['j'][keep], hic['p'][keep].astype(np.float64), np.zeros(len(keep)))
-    xyz_sm = np.ascontiguousarray(pop['coordinates'][:, :30].transpose(1, 0, 2))  # (S, nbead, 3) struct-major
+    xyz_sm = np.ascontiguousarray(pop['coordinates'][:, :32].transpose(1, 0, 2))  # (S, nbead, 3) struct-major
     return pop, pairs, xyz_sm
 
 
@@ -47,16 +47,19 @@ def _worker(rank, world, port, out):
         full = pipeline.gather_population(local).numpy()
         assert np.array_equal(full, xyz_sm)
         bead_major = np.ascontiguousarray(full.transpose(1, 0, 2))
-        lo, hi = pipeline.shard(len(pairs), rank, world)
+        combos = pipeline.pair_combos(pairs, pop['copy_ptr'], pop['chrom'][:len(pop['copy_ptr']) - 1])
+        spans = [pipeline.shard_weighted(combos, r, world) for r in range(world)]
+        lo, hi = spans[rank]
         rows, _ = oracle.actdist(bead_major, pop['radii'], pop['copy_ptr'], pop['copy_idx'], pop['chrom'],
                                  pairs[lo:hi], 2.0, 1)
         u8 = torch.from_numpy(rows.view(np.uint8).copy())
-        allrows, n = pipeline.gather_rows(u8, len(rows), row_dtype.itemsize)
+        cap = max(int(combos[a:b].sum()) for a, b in spans)
+        allrows, n = pipeline.gather_rows(u8, len(rows), row_dtype.itemsize, cap)
         tot = pipeline.reduce_sum_f64([float(rank + 1), 2.0], torch.device('cpu'))
         if rank == 0:
             np.save(out, allrows.numpy())
             assert n * row_dtype.itemsize == allrows.numel()
-            assert tot.tolist() == [3.0, 4.0]
+            assert tot.tolist() == [world * (world + 1) / 2.0, 2.0 * world]
     finally:
         dist.destroy_process_group()
 
@@ -69,9 +72,32 @@ def test_shard_covers_everything():
             assert all(spans[k][1] == spans[k + 1][0] for k in range(world - 1))
 
 
-def test_two_rank_astep_rows_equal_single_rank(tmp_path):
+def test_weighted_pair_shards_balance_combinations():
+    """contiguous pair shards of (nearly) equal distance combinations --
+    an inter pair of diploid loci is 4 combinations, an intra pair 2 -- covering every
+    pair once in CSR order."""
+    pop = np.load(os.path.join(GOLDEN, 'demo_population.npz'))
+    hic = np.load(os.path.join(GOLDEN, 'demo_hic_pairs.npz'))
+    pairs = make_pairs(hic['i'], hic['j'], hic['p'].astype(np.float64), np.zeros(len(hic['i'])))
+    hap = pop['chrom'][:len(pop['copy_ptr']) - 1]
+    w = pipeline.pair_combos(pairs, pop['copy_ptr'], hap)
+    nc = np.diff(pop['copy_ptr'])
+    assert set(np.unique(w)) <= {1, 2, 4}
+    assert np.all(w[hap[pairs['i']] != hap[pairs['j']]] == (nc[pairs['i']] * nc[pairs['j']])[hap[pairs['i']] != hap[pairs['j']]])
+    for world in (1, 2, 3, 4, 8):
+        spans = [pipeline.shard_weighted(w, r, world) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == len(w)
+        assert all(spans[k][1] == spans[k + 1][0] for k in range(world - 1))
+        loads = [int(w[a:b].sum()) for a, b in spans]
+        assert max(loads) - min(loads) <= 2 * w.max(), loads
+    assert pipeline.shard_weighted(np.zeros(0, np.int64), 0, 4) == (0, 0)
+    assert [pipeline.shard_weighted([4], r, 2) for r in range(2)] == [(0, 1), (1, 1)]
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_multi_rank_astep_rows_equal_single_rank(tmp_path, world):
     out = str(tmp_path / 'rows.npy')
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     got = np.load(out)
     pop, pairs, xyz_sm = _inputs()
     ref, _ = oracle.actdist(np.ascontiguousarray(xyz_sm.transpose(1, 0, 2)), pop['radii'], pop['copy_ptr'],
@@ -100,12 +126,16 @@ def _de_worker(rank, world, port, out):
         lo, hi = pipeline.shard(len(loci), rank, world)
         rows = A.damid_actdist(bm, pop['radii'], pop['copy_ptr'], pop['copy_idx'], loci[lo:hi], prof,
                                np.zeros(nhap, np.float32), 1, 0.05, 'sphere', 5500.0)
-        allrows, n = pipeline.gather_rows(torch.from_numpy(rows.view(np.uint8).copy()), len(rows), 12)
+        allrows, n = pipeline.gather_rows(torch.from_numpy(rows.view(np.uint8).copy()), len(rows), 12,
+                                          max(b - a for a, b in (pipeline.shard(len(loci), r, world)
+                                                                  for r in range(world))) * 2 * S)
         probes = loci[:40]
         t = np.sort(np.random.default_rng(2).lognormal(7.5, 0.4, (len(probes), S)), axis=1).astype(np.float32)
         plo, phi = pipeline.shard(len(probes), rank, world)
         omin, _, _, _ = A.fish_radial(bm, pop['copy_ptr'], pop['copy_idx'], probes[plo:phi], t[plo:phi], t[plo:phi])
-        allf, nf = pipeline.gather_rows(torch.from_numpy(omin.view(np.uint8).ravel().copy()), len(omin), 4 * S)
+        allf, nf = pipeline.gather_rows(torch.from_numpy(omin.view(np.uint8).ravel().copy()), len(omin), 4 * S,
+                                        max(b - a for a, b in (pipeline.shard(len(probes), r, world)
+                                                                for r in range(world))))
         if rank == 0:
             np.savez(out, damid=allrows.numpy(), fish=allf.numpy())
     finally:

@@ -1,4 +1,4 @@
-"""The world>1 branches of AMIteration actually running: two ranks on
+"""The world>1 branches of AMIteration actually running: two and four ranks on
 cuda:0 over gloo (torch.distributed.run, host-staged collectives) against one rank
 doing everything.  The A-step rows gathered in CSR order, every structure's Hi-C
 bonds, final coordinates, optimisation info and violation records, and the
@@ -26,13 +26,14 @@ def _free_port():
     return port
 
 
-def test_gpu_two_ranks_equal_one_rank(tmp_path):
+@pytest.mark.parametrize('world', [2, 4])
+def test_gpu_ranks_equal_one_rank(tmp_path, world):
     env = dict(os.environ, IGM_DIST_OUT=str(tmp_path), OMP_NUM_THREADS='2')
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=%d' % world,
            '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'dist_am_worker.py')]
     r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-4000:]
-    parts = [np.load(str(tmp_path / ('rank%d.npz' % k))) for k in range(2)]
+    parts = [np.load(str(tmp_path / ('rank%d.npz' % k))) for k in range(world)]
     inp = I.inputs()
     it = I.iteration(inp, 'cuda:0', 0, inp['xyz'].shape[0])
     it.astep()

@@ -11,7 +11,7 @@ import mstep_fixtures as F
 from igm_amd import model as M
 from igm_amd import synthetic as syn
 from igm_amd import _lib
-from igm_amd._lib import IGM_MSTEP_ENGINE_DD, IGM_MSTEP_FORCE_GLOBAL
+from igm_amd._lib import IGM_MSTEP_FORCE_GLOBAL
 
 pytestmark = pytest.mark.gpu
 
@@ -139,22 +139,6 @@ def model200():
     return atoms, poly, prm, ptr, sb, x
 
 
-def engine(prm, name):
-    """params for the HBM-size engine `name`: 'pop' (multi-kernel population engine,
-    the default) or 'dd' (domain-decomposed LDS engine)"""
-    p = _lib.MStepParams.from_buffer_copy(prm)
-    if name == 'dd':
-        p.flags |= IGM_MSTEP_ENGINE_DD
-    return p
-
-
-def assert_engine(name):
-    """the engine that ran the last anneal of HBM-size structures"""
-    st = _lib.context(0).engine_stats()
-    assert st['abort'] == (0 if name == 'dd' else -1), st
-    return st
-
-
 def test_gpu_200kb_forces_match_oracle(ms, model200):
     atoms, poly, prm, ptr, sb, x = model200
     assert atoms.nbead == 29838
@@ -162,20 +146,16 @@ def test_gpu_200kb_forces_match_oracle(ms, model200):
     fo, eo = oracle.mstep_forces(prm, x, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2)
     assert np.abs(fg - fo).max() <= 1e-6 * np.abs(fo).max() + 1e-6
     assert np.allclose(eg[:, :4], eo[:, :4], rtol=1e-9, atol=1e-9)
-    for name in ('dd', 'pop'):  # the f32 MD force path of both HBM-size engines
-        f32, _ = ms.forces(engine(prm, name), x, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2, f32=True)
-        assert_engine(name)
-        err = np.linalg.norm(f32 - fo, axis=2)
-        assert np.linalg.norm(err) <= 1e-5 * np.linalg.norm(np.linalg.norm(fo, axis=2))
+    # the f32 MD force path of the population engine
+    f32, _ = ms.forces(prm, x, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2, f32=True)
+    err = np.linalg.norm(f32 - fo, axis=2)
+    assert np.linalg.norm(err) <= 1e-5 * np.linalg.norm(np.linalg.norm(fo, axis=2))
 
 
-@pytest.mark.parametrize('name', ['dd', 'pop'])
-def test_gpu_200kb_md_segment_tracks_oracle(ms, model200, name):
+def test_gpu_200kb_md_segment_tracks_oracle(ms, model200):
     atoms, poly, prm, ptr, sb, x = model200
     v = np.stack([oracle.velocity_create(atoms.flags, 50.0, 21 + s) for s in range(2)]).astype(np.float32)
-    xg, vg = ms.md(engine(prm, name), x, v, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2, 50.0, 40.0, 1000.0,
-                   10)
-    assert_engine(name)
+    xg, vg = ms.md(prm, x, v, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2, 50.0, 40.0, 1000.0, 10)
     xo, vo = oracle.mstep_md(prm, x.astype(np.float64), v.astype(np.float64), atoms.radii, atoms.flags, poly, ptr,
                              sb, 0.5, 1.2, 50.0, 40.0, 1000.0, 10)
     moved = np.abs(xo - x).max()
