@@ -716,6 +716,20 @@ __device__ __noinline__ void pair_walk(int a, T xi, T yi, T zi, T ri, const vec4
     if (EN) ep += e;
 }
 
+// the same for the f32 MD force path, returning the force by value: a reference to
+// the caller's accumulators would make them escape into this out-of-line call and
+// live in scratch memory for the whole force routine (every bond's `fx +=` a scratch
+// load and store)
+__device__ __noinline__ float4 pair_walk_md(int a, float4 p0, const float4* pos, NList<float, uint16_t> L, float bx,
+                                            float by, float bz, const DevParams& P, float evf) {
+    float gx = 0.0f, gy = 0.0f, gz = 0.0f;
+    double e = 0.0;
+    walk27(cell_index<float>(bx, by, bz, L.gp, L.gp + 3, L.gn), L.cell, L.sorted, L.gn, [&](int j, bool ok) {
+        if (ok && j != a) pair_one<float, false>(j, p0.x, p0.y, p0.z, p0.w, pos, P, evf, gx, gy, gz, e);
+    });
+    return make_float4(gx, gy, gz, 0.0f);
+}
+
 // the bonds of one atom from the HBM adjacency (B.g, B.gt; B.n entries)
 template <typename T, bool EN>
 __device__ __forceinline__ void hbm_bonds(T xi, T yi, T zi, const vec4_t<T>* pos, const BondView& B, T& fx, T& fy,
@@ -859,7 +873,10 @@ __device__ __forceinline__ void atom_force_md(int s, int a, const float4& p0, ui
     if (ri >= 0.0f) {
         const int nn = L.nnb[a];
         if (nn == kNnbWalk) {
-            pair_walk<float, false, uint16_t>(a, xi, yi, zi, ri, pos, L, bx, by, bz, P, evf, fx, fy, fz, unused);
+            const float4 w = pair_walk_md(a, p0, pos, L, bx, by, bz, P, evf);
+            fx = w.x;
+            fy = w.y;
+            fz = w.z;
         } else if (nn > 0) {
             // slots k0..k0+U-1 are always readable (LDS: kl is a multiple of U; HBM: the
             // overflow regions carry U-1 slack slots); a slot past n holds a stale or
@@ -980,6 +997,7 @@ struct AnnealArgs {
     unsigned long long* prof;  // optional: cycles {build, force, rest, steps, builds} summed over structures
     float* forces_out;   // forces at the end (B, natom, 3), may be null
     int mode;            // 0: full protocol, 1: one MD segment from vel
+    int prune;           // LDS kernel: bond pruning on (IGM_BOND_PRUNE=0 turns it off: a test switch)
     int nseg;
     // per segment (mode 0) or the single segment (mode 1)
     int seg_steps[2 * IGM_MAX_STAGES];
@@ -1026,21 +1044,29 @@ __device__ __forceinline__ void kick_limit(float& vx, float& vy, float& vz, floa
     }
 }
 
-// element b (runtime, uniform per loop trip) of a per-thread register array
+// element b (runtime, uniform per loop trip) of a per-thread register array.  Each
+// element passes through an empty asm first: a select of plain loads would be folded
+// into ONE load from a selected address, i.e. a dynamically indexed array, which
+// the compiler then keeps in scratch memory (it did: xb and the bond masks of
+// anneal_kernel lived in scratch, read every step of the force loop).
+template <typename X>
+__device__ __forceinline__ X opaque(X x) {
+    uint32_t u = __builtin_bit_cast(uint32_t, x);
+    asm("" : "+v"(u));
+    return __builtin_bit_cast(X, u);
+}
 template <int BPT, typename X>
 __device__ __forceinline__ X pick(const X (&arr)[BPT], int b) {
-    X r = arr[0];
+    X r = opaque(arr[0]);
 #pragma unroll
-    for (int i = 1; i < BPT; ++i)
-        if (b == i) r = arr[i];
+    for (int i = 1; i < BPT; ++i) r = b == i ? opaque(arr[i]) : r;
     return r;
 }
 template <int BPT>
 __device__ __forceinline__ float pick(const float (&arr)[BPT][3], int b, int d) {
-    float r = arr[0][d];
+    float r = opaque(arr[0][d]);
 #pragma unroll
-    for (int i = 1; i < BPT; ++i)
-        if (b == i) r = arr[i][d];
+    for (int i = 1; i < BPT; ++i) r = b == i ? opaque(arr[i][d]) : r;
     return r;
 }
 
@@ -1173,7 +1199,7 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                         xb[b][1] = p.y;
                         xb[b][2] = p.z;
                         bmk[b] = 0xffffffffu;
-                        if (kBondPrune && lds_bonds && a < natom)
+                        if (kBondPrune && A.prune && lds_bonds && a < natom)
                             bmk[b] = bond_candidates(p, sm.rest + sm.boff[a], (int)sm.boff[a + 1] - (int)sm.boff[a],
                                                      sm.btab, sm.pos, skin);
                     }
@@ -1196,12 +1222,11 @@ __global__ void __launch_bounds__(NT) anneal_kernel(AnnealArgs A) {
                                                      pick<BPT>(xb, b, 2), B, A.P, evf, envf, fx, fy, fz,
                                                      natom - 1, pick<BPT>(bmk, b));
 #pragma unroll
-                        for (int i = 0; i < BPT; ++i)
-                            if (b == i) {
-                                f[i][0] = fx;
-                                f[i][1] = fy;
-                                f[i][2] = fz;
-                            }
+                        for (int i = 0; i < BPT; ++i) {  // (unconditional selects: no store to a selected address)
+                            f[i][0] = b == i ? fx : f[i][0];
+                            f[i][1] = b == i ? fy : f[i][1];
+                            f[i][2] = b == i ? fz : f[i][2];
+                        }
                     }
                 }
                 if (A.prof) {
@@ -1318,6 +1343,90 @@ constexpr bool kPopFused = IGM_POP_FUSED != 0;
 #endif
 constexpr int kPopOuterCap = IGM_POP_OUTER_CAP;  // outer-list entries per slot (two-level lists)
 constexpr int kPopListRow = kPopListCap + 2;  // u16 per LDS list row of the build (odd word stride)
+#ifndef IGM_POP_BRICK
+#define IGM_POP_BRICK 0
+#endif
+// Slot order of the population engine: the cells of a structure's grid ordered x-fastest
+// (0), or in bricks of B x B x B cells (B = IGM_POP_BRICK), the bricks x-fastest and the
+// cells inside a brick x-fastest, so that 64 or 256 consecutive slots are a compact blob
+// of space instead of a thin rod along x (the neighbour gathers of a wave touch fewer
+// cache lines); a 3-cell x-run of the list build then straddles at most one brick edge.
+constexpr int kBrick = IGM_POP_BRICK;
+
+// index of cell (cx, cy, cz) in the slot order of a grid of nb[3] cells
+__device__ __forceinline__ int pop_cell_of(int cx, int cy, int cz, const int* nb) {
+    if constexpr (kBrick == 0) {
+        return (cz * nb[1] + cy) * nb[0] + cx;
+    } else {
+        constexpr int B = kBrick;
+        const int nbx = (nb[0] + B - 1) / B, nby = (nb[1] + B - 1) / B;
+        return (((cz / B) * nby + cy / B) * nbx + cx / B) * (B * B * B) + ((cz % B) * B + cy % B) * B + cx % B;
+    }
+}
+// size of the cell index space of a grid (bricks: whole bricks; the ranks of cells
+// outside the grid stay empty)
+__host__ __device__ __forceinline__ int pop_ncell(const int* nb) {
+    if constexpr (kBrick == 0) {
+        return nb[0] * nb[1] * nb[2];
+    } else {
+        constexpr int B = kBrick;
+        return ((nb[0] + B - 1) / B * B) * ((nb[1] + B - 1) / B * B) * ((nb[2] + B - 1) / B * B);
+    }
+}
+// the cell coordinates of a position (clamped into the grid, as cell_index)
+__device__ __forceinline__ void pop_cell_xyz(float x, float y, float z, const float* lo, const float* inv,
+                                             const int* nb, int& cx, int& cy, int& cz) {
+    const float pp[3] = {x, y, z};
+    int ci[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const int v = (int)((pp[d] - lo[d]) * inv[d]);
+        ci[d] = v < 0 ? 0 : (v >= nb[d] ? nb[d] - 1 : v);
+    }
+    cx = ci[0];
+    cy = ci[1];
+    cz = ci[2];
+}
+__device__ __forceinline__ int pop_cell_index(float x, float y, float z, const float* lo, const float* inv,
+                                              const int* nb) {
+    int cx, cy, cz;
+    pop_cell_xyz(x, y, z, lo, inv, nb, cx, cy, cz);
+    return pop_cell_of(cx, cy, cz, nb);
+}
+// The slot runs of the 27 cells around (cx, cy, cz): per (y, z) row the x-run of up to
+// 3 cells -- one run, or with bricks two where the run straddles a brick edge (the
+// second empty otherwise); rows outside the grid are empty.  Run r of row k is index
+// k * kRunsPerRow + r.  cell[] holds the first slot of every cell index (and the end
+// of the last one), so cell index c's slots are [cell[c], cell[c + 1]).
+constexpr int kRunsPerRow = kBrick ? 2 : 1;
+__device__ __forceinline__ void pop_runs(int cx, int cy, int cz, const int* cell, const int* nb,
+                                         int (&rb)[9 * kRunsPerRow], int (&re)[9 * kRunsPerRow]) {
+    const int nx = nb[0], ny = nb[1], nz = nb[2];
+    const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+        const int z0 = cz + r / 3 - 1, y0 = cy + r % 3 - 1;
+        const bool ok = z0 >= 0 && z0 < nz && y0 >= 0 && y0 < ny;
+        if constexpr (kBrick == 0) {
+            const int rw = ok ? (z0 * ny + y0) * nx : 0;
+            rb[r] = ok ? cell[rw + xlo] : 0;
+            re[r] = ok ? cell[rw + xhi + 1] : 0;
+        } else {
+            constexpr int B = kBrick;
+            const int zz = ok ? z0 : 0, yy = ok ? y0 : 0;
+            const int xm = xhi / B * B;  // the first x of xhi's brick
+            const bool split = xlo < xm;
+            const int a0 = pop_cell_of(xlo, yy, zz, nb);
+            const int a1 = pop_cell_of(split ? xm - 1 : xhi, yy, zz, nb);
+            const int b0 = pop_cell_of(xm, yy, zz, nb);
+            const int b1 = pop_cell_of(xhi, yy, zz, nb);
+            rb[2 * r] = ok ? cell[a0] : 0;
+            re[2 * r] = ok ? cell[a1 + 1] : 0;
+            rb[2 * r + 1] = ok && split ? cell[b0] : 0;
+            re[2 * r + 1] = ok && split ? cell[b1 + 1] : 0;
+        }
+    }
+}
 
 struct PopBuf {
     float4* pos;   // (B, ldn): x, y, z, w = radius (bead) or -(radius + 1)
@@ -1615,10 +1724,19 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
         if (vol / (cs * cs * cs) > cap) cs = cbrtf(vol / cap) * 1.0001f;
         float* gp = A.gp + (size_t)s * 8;
         int* gn = A.gn + (size_t)s * 8;
+        int nbv[3];
+        for (;;) {  // (bricks: whole bricks must fit the cap too)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                nbv[d] = (int)floorf(ext[d] / cs);
+                if (nbv[d] < 1) nbv[d] = 1;
+            }
+            if (kBrick == 0 || pop_ncell(nbv) <= A.ccap) break;
+            cs *= 1.02f;
+        }
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            int nbd = (int)floorf(ext[d] / cs);
-            if (nbd < 1) nbd = 1;
+            const int nbd = nbv[d];
             sg[d] = -mm[d];
             sg[3 + d] = ext[d] > 0.0f ? (float)nbd / ext[d] : 0.0f;
             sn[d] = nbd;
@@ -1630,7 +1748,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
     __syncthreads();
     const float lo[3] = {sg[0], sg[1], sg[2]}, inv[3] = {sg[3], sg[4], sg[5]};
     const int nb[3] = {sn[0], sn[1], sn[2]};
-    const int ncell = nb[0] * nb[1] * nb[2];
+    const int ncell = pop_ncell(nb);
     const int nw = (ncell + 3) >> 1;  // words holding the cells 0..ncell+1
     uint16_t* ids = reinterpret_cast<uint16_t*>(cw + ((A.ccap + 3) >> 1));
     for (int k = t; k < nw; k += kPopSortNT) cw[k] = 0u;
@@ -1651,7 +1769,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
             for (int u = 0; u < 8; ++u) {
                 const int i = t + (u0 + u) * kPopSortNT;
                 if (u0 + u < APT && i < N) {
-                    const int c = pp[u].w >= 0.0f ? cell_index<float>(pp[u].x, pp[u].y, pp[u].z, lo, inv, nb) : ncell;
+                    const int c = pp[u].w >= 0.0f ? pop_cell_index(pp[u].x, pp[u].y, pp[u].z, lo, inv, nb) : ncell;
                     const uint32_t sh = (uint32_t)(c & 1) << 4;
                     const uint32_t old = atomicAdd(&cw[c >> 1], 1u << sh);
                     cr[u0 + u] = ((uint32_t)c << 16) | ((old >> sh) & 0xffffu);
@@ -1670,7 +1788,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
         for (int u = 0; u < U; ++u) {
             const int i = i0 + u * kPopSortNT;
             if (i >= N) break;
-            const int c = pp[u].w >= 0.0f ? cell_index<float>(pp[u].x, pp[u].y, pp[u].z, lo, inv, nb) : ncell;
+            const int c = pp[u].w >= 0.0f ? pop_cell_index(pp[u].x, pp[u].y, pp[u].z, lo, inv, nb) : ncell;
             const uint32_t sh = (uint32_t)(c & 1) << 4;
             const uint32_t old = atomicAdd(&cw[c >> 1], 1u << sh);
             slotn[i] = (int)(((uint32_t)c << 16) | ((old >> sh) & 0xffffu));
@@ -1889,27 +2007,20 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
     const float* gp = A.gp + (size_t)s * 8;
     const int* gn = A.gn + (size_t)s * 8;
     const int* cell = A.cell + (size_t)s * kPopCells;
-    const int nx = gn[0], ny = gn[1], nz = gn[2];
     const int kcap = 4 * T.kq;  // <= kPopListCap
     uint16_t* lst = reinterpret_cast<uint16_t*>(row);
     const float cut2 = A.P.cut_list * A.P.cut_list;
     int k = 0;
-    // The 27 cells are 9 x-runs of slots.  All 18 run bounds are loaded together,
-    // then each z-layer's 3 runs a batch of kFillW slots per run at once (the rare
-    // longer run finishes in a loop): 4 dependent memory round trips per slot in
-    // place of one per run and per batch.
-    const int c = cell_index<float>(p0.x, p0.y, p0.z, gp, gp + 3, gn);
-    const int cx = c % nx, cy = (c / nx) % ny, cz = c / (nx * ny);
-    const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
-    int rb[9], re[9];
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-        const int z0 = cz + r / 3 - 1, y0 = cy + r % 3 - 1;
-        const bool ok = z0 >= 0 && z0 < nz && y0 >= 0 && y0 < ny;
-        const int rw = ok ? (z0 * ny + y0) * nx : 0;
-        rb[r] = ok ? cell[rw + xlo] : 0;
-        re[r] = ok ? cell[rw + xhi + 1] : 0;
-    }
+    // The 27 cells are 9 x-runs of slots (with bricks up to 18: a run straddling a
+    // brick edge is two).  All run bounds are loaded together, then each z-layer's
+    // runs a batch of kFillW slots per run at once (the rare longer run finishes in a
+    // loop): 4 dependent memory round trips per slot in place of one per run and batch.
+    int cx, cy, cz;
+    pop_cell_xyz(p0.x, p0.y, p0.z, gp, gp + 3, gn, cx, cy, cz);
+    constexpr int NR = 9 * kRunsPerRow, RL = NR / 3;  // runs, runs per z-layer
+    constexpr int FW = kBrick ? 2 : kFillW;           // (loads in flight per layer: RL * FW)
+    int rb[NR], re[NR];
+    pop_runs(cx, cy, cz, cell, gn, rb, re);
     const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
     auto test = [&](int j, const float3& p) {
         const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
@@ -1919,21 +2030,21 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
     };
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
-        float3 pp[3][kFillW];
-        int jj[3][kFillW];
+        float3 pp[RL][FW];
+        int jj[RL][FW];
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+        for (int r = 0; r < RL; ++r)
 #pragma unroll
-            for (int u = 0; u < kFillW; ++u) {
-                const int j = rb[3 * g + r] + u;
-                jj[r][u] = j < re[3 * g + r] ? j : i;  // past the run: the slot itself (never listed)
+            for (int u = 0; u < FW; ++u) {
+                const int j = rb[RL * g + r] + u;
+                jj[r][u] = j < re[RL * g + r] ? j : i;  // past the run: the slot itself (never listed)
                 pp[r][u] = pop_ld3(rp, jj[r][u]);
             }
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
+        for (int r = 0; r < RL; ++r) {
 #pragma unroll
-            for (int u = 0; u < kFillW; ++u) test(jj[r][u], pp[r][u]);
-            for (int j = rb[3 * g + r] + kFillW; j < re[3 * g + r]; ++j) test(j, pop_ld3(rp, j));
+            for (int u = 0; u < FW; ++u) test(jj[r][u], pp[r][u]);
+            for (int j = rb[RL * g + r] + FW; j < re[RL * g + r]; ++j) test(j, pop_ld3(rp, j));
         }
     }
     // the last quad padded with the slot itself: a zero-distance entry adds no force
@@ -2040,15 +2151,20 @@ __global__ void __launch_bounds__(kPopBS) pop_refilter_kernel(PopArgs A) {
 __device__ __noinline__ float4 pop_walk_pairs(const float4* pos, const int* cell, const float* gp, const int* gn,
                                               float bx, float by, float bz, int i, float4 p0, float evfpi) {
     float fx = 0.0f, fy = 0.0f, fz = 0.0f;
-    walk27(cell_index<float>(bx, by, bz, gp, gp + 3, gn), cell, (const uint16_t*)nullptr, gn, [&](int j, bool ok) {
-        const float4 p = pos[j];
-        const float dx = p0.x - p.x, dy = p0.y - p.y, dz = p0.z - p.z;
-        const float f = soft_pair_bf(dx * dx + dy * dy + dz * dz, p0.w + p.w, evfpi);
-        const float m = (ok && j != i) ? f : 0.0f;
-        fx += m * dx;
-        fy += m * dy;
-        fz += m * dz;
-    });
+    int cx, cy, cz;
+    pop_cell_xyz(bx, by, bz, gp, gp + 3, gn, cx, cy, cz);
+    int rb[9 * kRunsPerRow], re[9 * kRunsPerRow];
+    pop_runs(cx, cy, cz, cell, gn, rb, re);
+    for (int r = 0; r < 9 * kRunsPerRow; ++r)
+        for (int j = rb[r]; j < re[r]; ++j) {
+            const float4 p = pos[j];
+            const float dx = p0.x - p.x, dy = p0.y - p.y, dz = p0.z - p.z;
+            const float f = soft_pair_bf(dx * dx + dy * dy + dz * dz, p0.w + p.w, evfpi);
+            const float m = j != i ? f : 0.0f;
+            fx += m * dx;
+            fy += m * dy;
+            fz += m * dz;
+        }
     return make_float4(fx, fy, fz, 0.0f);
 }
 
@@ -2106,6 +2222,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     // padding entries, which are the slot itself) finite, and it is below one ulp of
     // every r2 that is not zero.
     pop_f2 ax = {0.0f, 0.0f}, ay = {0.0f, 0.0f}, az = {0.0f, 0.0f};
+    float bfx = 0.0f, bfy = 0.0f, bfz = 0.0f;  // the bonds' sum
     auto pair2 = [&](const float4& a, const float4& b) {
         const pop_f2 dx = pop_f2{xi, xi} - pop_f2{a.x, b.x}, dy = pop_f2{yi, yi} - pop_f2{a.y, b.y},
                      dz = pop_f2{zi, zi} - pop_f2{a.z, b.z};
@@ -2129,9 +2246,9 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         const float dr = r2 * rinv - c.x;
         const bool active = (e & kLowerBit) ? (dr < 0.0f) : (dr > 0.0f);
         const float m = (on && active && r2 > 0.0f) ? -2.0f * c.y * dr * rinv : 0.0f;
-        fx += m * dx;
-        fy += m * dy;
-        fz += m * dz;
+        bfx += m * dx;
+        bfy += m * dy;
+        bfz += m * dz;
     };
     if (ri >= 0.0f) {
         if (nn == kNnbWalk) {
@@ -2177,33 +2294,12 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
                     for (int u = 0; u < 2 * U; ++u) pair2(pt[2 * u], pt[2 * u + 1]);
                 }
             };
-#ifdef IGM_POP_TIMING_PAIR_REPS  // timing variants only: the pair loop repeated, the repeats discarded
-            pop_f2 kx, ky, kz;
-            for (int rep = 0; rep < IGM_POP_TIMING_PAIR_REPS; ++rep) {
-#endif
             pairs([&](uint32_t j) { return pop_ld(rp, j); });
-#ifdef IGM_POP_TIMING_PAIR_REPS
-                if (rep == 0) {
-                    kx = ax;
-                    ky = ay;
-                    kz = az;
-                }
-            }
-            if (A.cm.natom >= 0) {
-                ax = kx;
-                ay = ky;
-                az = kz;
-            }
-#endif
             fx = ax.x + ax.y;
             fy = ay.x + ay.y;
             fz = az.x + az.y;
         }
     }
-#ifdef IGM_POP_TIMING_BOND_REPS  // timing variants only: the bond loop repeated, the repeats discarded
-    float kfx = 0.0f, kfy = 0.0f, kfz = 0.0f;
-    for (int rep = 0; rep < IGM_POP_TIMING_BOND_REPS; ++rep) {
-#endif
     for (int k0 = 0; k0 < deg; k0 += 4) {
         uint32_t et[4];
         if (rebuilt) {  // atom-space entries -> slot-space (the permute of the unfused engine)
@@ -2237,19 +2333,9 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 #pragma unroll
         for (int u = 0; u < 4; ++u) bond(pt[u], ct[u], et[u], k0 + u < deg);
     }
-#ifdef IGM_POP_TIMING_BOND_REPS
-        if (rep == 0) {
-            kfx = fx;
-            kfy = fy;
-            kfz = fz;
-        }
-    }
-    if (A.cm.natom >= 0) {
-        fx = kfx;
-        fy = kfy;
-        fz = kfz;
-    }
-#endif
+    fx += bfx;
+    fy += bfy;
+    fz += bfz;
     // envelopes (non-bead atoms carry -(radius + 1))
     const float rad = ri >= 0.0f ? ri : -ri - 1.0f;
     for (int e = 0; e < A.P.nenv; ++e) {
@@ -3786,6 +3872,10 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
             while (*q && *q != ',') ++q;
             if (*q == ',') ++q;
         }
+    }
+    {
+        const char* e = getenv("IGM_BOND_PRUNE");
+        A.prune = e ? atoi(e) != 0 : 1;
     }
     IGM_HIP_CHECK(c, hipMemsetAsync(pr.cm.work_counter, 0, sizeof(int), c->stream));
     if (getenv("IGM_PROF")) {

@@ -109,3 +109,63 @@ def test_gpu_200kb_protocol_matches_oracle_and_reruns_bitwise():
     assert ok, pv
     assert np.all(ig['temp'] < 1.0)
     assert np.all(io['temp'] < 1.0)
+
+
+def test_gpu_200kb_full_protocol_on_astep_bonds_matches_oracle():
+    """The bench's own workload, at FULL protocol (lammps.py:285-356: 4 stages + relax,
+    47 008 MD steps, CG): a 200 kb population runs one warmup A/M iteration on the GPU
+    (AMIteration: Hi-C A-step over the population, Hi-C selection, anneal + CG); from
+    that state (AMIteration.snapshot) the next iteration's A-step and selection give
+    every structure its Hi-C restraints, and 16 structures then run the whole protocol
+    on the GPU engine and in the fp64 oracle with the same coordinates, restraints and
+    LAMMPS seeds.  The KS statistic of tests/mstep_stats.py does not separate the two
+    populations on E_pair, E_bond, E_env, E_total per bead, the violation fraction and
+    the final Temp; the GPU rerun is bitwise identical.  Prints the oracle's wall time
+    (a full-protocol CPU measurement of config C on this host's threads)."""
+    import time
+    import torch
+    from igm_amd import mstep
+    from igm_amd.pipeline import AMIteration
+    from igm_amd._lib import bond_dtype
+    S, n = 32, 16
+    pop = syn.population_200kb(S, first_sid=0)
+    atoms = M.Atoms(pop['radii'])
+    x = np.zeros((S, atoms.n, 3), np.float32)
+    x[:, :atoms.nbead] = pop['xyz']
+    chrom = np.concatenate([pop['chrom'], [-1]]).astype(np.int32)
+    poly = M.polymer_bonds(pop['chrom'], pop['copy'], pop['radii'], 2.0, 1.0)
+    prm = M.params_from_cfg({'optimization': {'optimizer_options': json.loads(json.dumps(syn.DEMO_PROTOCOL))}},
+                            [((5500.0,) * 3, 1.0)])
+    i, j, p = syn.hic_pairs_200kb(0.01)
+    pairs = np.zeros(len(i), pair_dtype)
+    pairs['i'], pairs['j'], pairs['pwish'] = i, j, p
+    dev = torch.device('cuda', 0)
+    it = AMIteration(dev, x, atoms, chrom, pop['copy_ptr'], pop['copy_idx'], pairs, prm, poly)
+    it.step()  # the warmup A/M iteration
+    snap = it.snapshot()
+    it.load_snapshot(snap)
+    it.astep()
+    it.select()
+    torch.cuda.synchronize(dev)
+    ptr = it.hic_ptr.cpu().numpy()[:n + 1].copy()
+    sb = it.hic_bonds.cpu().numpy().view(bond_dtype)[:ptr[-1]].copy()
+    x0 = np.ascontiguousarray(snap['xyz'].cpu().numpy()[:n])
+    seeds = M.lammps_seeds(it.seed, it.sids[:n], snap['step_no'])
+    del it, snap
+    torch.cuda.empty_cache()
+    assert ptr[-1] > 1000 * n  # thousands of A-step-selected Hi-C bonds per structure
+    xg, ig = mstep.run(prm, x0, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
+    xg2, ig2 = mstep.run(prm, x0, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
+    assert np.array_equal(xg, xg2) and ig.tobytes() == ig2.tobytes()  # bitwise reproducible
+    assert np.all(np.isfinite(xg)) and np.all(ig['final_energy'] < ig['einitial'])
+    t0 = time.perf_counter()
+    xo, io, _ = oracle.mstep_run(prm, x0.copy(), atoms.radii, atoms.flags, poly, ptr, sb, seeds, nthreads=16)
+    print('[oracle] config C full protocol: %d structures on 16 threads in %.1f s' % (n, time.perf_counter() - t0))
+    so = MS.population_stats(io, xo, poly, ptr, sb, atoms.nbead)
+    so['env'] = io['env_energy'][:, 0] / atoms.nbead
+    sg = MS.population_stats(ig, xg, poly, ptr, sb, atoms.nbead)
+    sg['env'] = ig['env_energy'][:, 0] / atoms.nbead
+    ok, pv = MS.same_population(sg, so, keys=('pair', 'bond', 'env', 'total', 'viol_frac', 'temp'))
+    print('[ks] p-values', pv)
+    assert ok, pv
+    assert np.all(ig['temp'] < 1.0) and np.all(io['temp'] < 1.0)

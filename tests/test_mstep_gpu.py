@@ -196,3 +196,22 @@ def test_gpu_violations_equal_reference(demo, ms):
             assert stats[s, c, 101] == rec['violated_restr']
             assert stats[s, c, 102] == rec['n_violations']
             assert stats[s, c, 103] == rec['n_imposed']
+
+
+def test_gpu_bond_pruning_is_bitwise_exact(demo, ms, monkeypatch):
+    """The LDS anneal kernel's bond pruning (bond_candidates: at each list build, the
+    bonds that cannot act before the next build are skipped) changes no bit: the same
+    config B batch (frustrated demo restraints, the whole protocol shape at 300 MD steps
+    per stage, default skins) with IGM_BOND_PRUNE=0 and with pruning on ends in the
+    same coordinates, energies, temperatures and rebuild counts."""
+    from test_mstep_stats import _inputs
+    sids = list(range(16))
+    atoms, poly, ptr, sb, x = _inputs(sids, 1000, 1000)
+    p = M.params_from_cfg({'optimization': {'optimizer_options': short_protocol()}}, [((5500.0,) * 3, 1.0)])
+    seeds = M.lammps_seeds(6535, sids, 7)
+    monkeypatch.setenv('IGM_BOND_PRUNE', '0')
+    x0, i0 = ms.run(p, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
+    monkeypatch.delenv('IGM_BOND_PRUNE')
+    x1, i1 = ms.run(p, x, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
+    assert np.array_equal(x0, x1) and i0.tobytes() == i1.tobytes()
+    assert np.all(i1['nrebuild'] > 10) and np.all(np.isfinite(x1))

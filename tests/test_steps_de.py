@@ -250,3 +250,67 @@ def test_random_init_reproduces_the_reference_draw_order(tmp_path):
         assert np.array_equal(x[:, sid], want)
     from igm_amd import hss
     assert np.isnan(hss.Hss(store.path).violation)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('config', ['D', 'E'])
+def test_gpu_config_chain_with_hip_kernels(tmp_path, config):
+    """The configuration D / E iteration of igm-run with optimization/kernel = 'hip'
+    (the product's HIP kernels behind every Step class igm-run instantiates for them,
+    bin/igm-run:139-167) beside the same chain on the CPU oracle kernels, from the same
+    files: the same steps and StepDB status rows; the A-step outputs (Hi-C actdist rows,
+    DamID rows, FISH and SPRITE assignments) byte-identical; the M-step ran on the GPU
+    (coordinates updated in place, the summary carries every restraint class)."""
+    make = _config_D if config == 'D' else _config_E
+    out = {}
+    for kind in ('oracle', 'hip'):
+        d = tmp_path / kind
+        d.mkdir()
+        cfg, _ = make(str(d))
+        if kind == 'hip':
+            cfg['optimization']['kernel'] = 'hip'
+        store = ST.PopulationStore(cfg['optimization']['structure_output'])
+        x0 = np.array(store.coordinates())
+        ran = _iteration(cfg)
+        db = ST.StepDB(cfg['parameters']['step_db'])
+        out[kind] = dict(cfg=cfg, names=[type(s).__name__ for s in ran], x0=x0, x1=np.array(store.coordinates()),
+                         status=[[r['status'] for r in db.get_history(s.uid)] for s in ran],
+                         summary=json.loads(store.read_summary()))
+        if config == 'E':
+            CK.oracle.set_volume(None)
+    o, h = out['oracle'], out['hip']
+    assert h['names'] == o['names'] and h['status'] == o['status']
+    assert all(st[-1] == 'completed' for st in h['status'])
+    ro = ST.read_rows(o['cfg']['runtime']['Hi-C']['actdist_file'])
+    rh = ST.read_rows(h['cfg']['runtime']['Hi-C']['actdist_file'])
+    assert len(rh) > 100 and rh.tobytes() == ro.tobytes()
+    if config == 'D':
+        do = ST.read_damid_rows(o['cfg']['runtime']['DamID']['damid_actdist_file'])
+        dh = ST.read_damid_rows(h['cfg']['runtime']['DamID']['damid_actdist_file'])
+        assert len(dh) > 0 and dh.tobytes() == do.tobytes()
+    else:
+        fo = ST._h5_tree(o['cfg']['runtime']['FISH']['fish_assignment_file'])
+        fh = ST._h5_tree(h['cfg']['runtime']['FISH']['fish_assignment_file'])
+        for k in ('radial_min', 'radial_max', 'pair_min', 'pair_max'):
+            assert np.array_equal(fh[k], fo[k]), k
+        so, sh = ST._h5_tree(ST.sprite_assignment_path(o['cfg'])), ST._h5_tree(ST.sprite_assignment_path(h['cfg']))
+        for k in ('assignment', 'selected', 'indptr'):
+            assert np.array_equal(sh[k], so[k]), k
+    assert np.all(np.isfinite(h['x1'])) and not np.array_equal(h['x0'], h['x1'])
+    assert set(h['summary']['byrestraint']) == set(o['summary']['byrestraint'])
+    assert 0.0 <= h['cfg']['runtime']['violation_score'] < 0.5
+
+
+def test_every_step_class_igm_run_instantiates_has_a_dropin():
+    """INTEGRATION.md 1b swaps every Step class bin/igm-run instantiates (:66-82 start-up,
+    :105-167 iteration) for igm_amd.steps' class of the same name: each exists, is a Step
+    with the reference's run() lifecycle, and igm_run's step lists use exactly them."""
+    names = ('RandomInit', 'PolymerAssignmentStep', 'RelaxInit', 'ActivationDistanceStep', 'FishAssignmentStep',
+             'SpriteAssignmentStep', 'DamidActivationDistanceStep', 'ModelingStep')
+    for n in names:
+        cls = getattr(ST, n)
+        assert issubclass(cls, ST.Step) and cls.__name__ == n and cls.run is ST.Step.run
+    used = {c.__name__ for c in RUN.iteration_steps({'restraints': {'Hi-C': {}, 'FISH': {}, 'sprite': {},
+                                                                    'DamID': {}, 'polymer': {}}})}
+    used |= {c.__name__ for c in RUN.startup_steps({'model': {'restraints': {}}})}
+    assert used == set(names)
