@@ -325,8 +325,9 @@ def bench_config_c(args, dev, world, rank, local, backend='nccl'):
                                'protocol%s' % (total, per, '' if args.protocol_scale == 1.0 else
                                                ' x%g (NOT the metric)' % args.protocol_scale),
                    'nstruct_total': total, 'nstruct_per_gpu': per, 'sigma': 0.01, 'npairs': int(it.npairs_total),
-                   'parallelism': 'structures sharded over %d ranks, A-step pair-sharded after an RCCL all-gather'
-                                  % world if world > 1 else 'one GPU'},
+                   'parallelism': 'structures sharded over %d ranks, A-step pair-sharded after an all-gather (%s)'
+                                  % (world, 'RCCL' if backend == 'nccl' else backend + ' rehearsal, not a measurement')
+                                  if world > 1 else 'one GPU'},
         'roofline': {'bound': 'hbm', 'kernel': 'population engine (pop_* kernels of every MD step)',
                      'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                      'traffic': traffic, 'traffic_source': traffic_src,

@@ -61,7 +61,7 @@ constexpr bool kBondPrune = IGM_BOND_PRUNE != 0;
 #endif
 constexpr int kPopPairBatch = IGM_POP_PAIR_BATCH;  // population engine: list quads whose loads are in flight together
 #ifndef IGM_POP_FORCE_OCC
-#define IGM_POP_FORCE_OCC 6  // waves per SIMD the force kernel's registers must allow (6 beats 4, 5 and 8)
+#define IGM_POP_FORCE_OCC 7  // waves per SIMD the force kernel's registers must allow (7: -1.0 % anneal against 6, which beat 4, 5 and 8)
 #endif
 
 // LDS anneal kernel: neighbours per batch.  LDS latency is short and lists are short, so
@@ -1343,36 +1343,13 @@ constexpr bool kPopFused = IGM_POP_FUSED != 0;
 #endif
 constexpr int kPopOuterCap = IGM_POP_OUTER_CAP;  // outer-list entries per slot (two-level lists)
 constexpr int kPopListRow = kPopListCap + 2;  // u16 per LDS list row of the build (odd word stride)
-#ifndef IGM_POP_BRICK
-#define IGM_POP_BRICK 0
-#endif
-// Slot order of the population engine: the cells of a structure's grid ordered x-fastest
-// (0), or in bricks of B x B x B cells (B = IGM_POP_BRICK), the bricks x-fastest and the
-// cells inside a brick x-fastest, so that 64 or 256 consecutive slots are a compact blob
-// of space instead of a thin rod along x (the neighbour gathers of a wave touch fewer
-// cache lines); a 3-cell x-run of the list build then straddles at most one brick edge.
-constexpr int kBrick = IGM_POP_BRICK;
-
-// index of cell (cx, cy, cz) in the slot order of a grid of nb[3] cells
+// index of cell (cx, cy, cz) in the slot order of a grid of nb[3] cells: x-fastest.
+// (Measured on config C, pop=1000: bricks of 2^3 or 4^3 cells -- 64 or 256 consecutive
+// slots a compact blob instead of a rod along x -- were 12 % and 13 % SLOWER)
 __device__ __forceinline__ int pop_cell_of(int cx, int cy, int cz, const int* nb) {
-    if constexpr (kBrick == 0) {
-        return (cz * nb[1] + cy) * nb[0] + cx;
-    } else {
-        constexpr int B = kBrick;
-        const int nbx = (nb[0] + B - 1) / B, nby = (nb[1] + B - 1) / B;
-        return (((cz / B) * nby + cy / B) * nbx + cx / B) * (B * B * B) + ((cz % B) * B + cy % B) * B + cx % B;
-    }
+    return (cz * nb[1] + cy) * nb[0] + cx;
 }
-// size of the cell index space of a grid (bricks: whole bricks; the ranks of cells
-// outside the grid stay empty)
-__host__ __device__ __forceinline__ int pop_ncell(const int* nb) {
-    if constexpr (kBrick == 0) {
-        return nb[0] * nb[1] * nb[2];
-    } else {
-        constexpr int B = kBrick;
-        return ((nb[0] + B - 1) / B * B) * ((nb[1] + B - 1) / B * B) * ((nb[2] + B - 1) / B * B);
-    }
-}
+__host__ __device__ __forceinline__ int pop_ncell(const int* nb) { return nb[0] * nb[1] * nb[2]; }
 // the cell coordinates of a position (clamped into the grid, as cell_index)
 __device__ __forceinline__ void pop_cell_xyz(float x, float y, float z, const float* lo, const float* inv,
                                              const int* nb, int& cx, int& cy, int& cz) {
@@ -1394,37 +1371,19 @@ __device__ __forceinline__ int pop_cell_index(float x, float y, float z, const f
     return pop_cell_of(cx, cy, cz, nb);
 }
 // The slot runs of the 27 cells around (cx, cy, cz): per (y, z) row the x-run of up to
-// 3 cells -- one run, or with bricks two where the run straddles a brick edge (the
-// second empty otherwise); rows outside the grid are empty.  Run r of row k is index
-// k * kRunsPerRow + r.  cell[] holds the first slot of every cell index (and the end
-// of the last one), so cell index c's slots are [cell[c], cell[c + 1]).
-constexpr int kRunsPerRow = kBrick ? 2 : 1;
-__device__ __forceinline__ void pop_runs(int cx, int cy, int cz, const int* cell, const int* nb,
-                                         int (&rb)[9 * kRunsPerRow], int (&re)[9 * kRunsPerRow]) {
+// 3 cells, one contiguous slot range (rows outside the grid are empty).  cell[] holds
+// the first slot of every cell (and the end of the last one).
+__device__ __forceinline__ void pop_runs(int cx, int cy, int cz, const int* cell, const int* nb, int (&rb)[9],
+                                         int (&re)[9]) {
     const int nx = nb[0], ny = nb[1], nz = nb[2];
     const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
         const int z0 = cz + r / 3 - 1, y0 = cy + r % 3 - 1;
         const bool ok = z0 >= 0 && z0 < nz && y0 >= 0 && y0 < ny;
-        if constexpr (kBrick == 0) {
-            const int rw = ok ? (z0 * ny + y0) * nx : 0;
-            rb[r] = ok ? cell[rw + xlo] : 0;
-            re[r] = ok ? cell[rw + xhi + 1] : 0;
-        } else {
-            constexpr int B = kBrick;
-            const int zz = ok ? z0 : 0, yy = ok ? y0 : 0;
-            const int xm = xhi / B * B;  // the first x of xhi's brick
-            const bool split = xlo < xm;
-            const int a0 = pop_cell_of(xlo, yy, zz, nb);
-            const int a1 = pop_cell_of(split ? xm - 1 : xhi, yy, zz, nb);
-            const int b0 = pop_cell_of(xm, yy, zz, nb);
-            const int b1 = pop_cell_of(xhi, yy, zz, nb);
-            rb[2 * r] = ok ? cell[a0] : 0;
-            re[2 * r] = ok ? cell[a1 + 1] : 0;
-            rb[2 * r + 1] = ok && split ? cell[b0] : 0;
-            re[2 * r + 1] = ok && split ? cell[b1 + 1] : 0;
-        }
+        const int rw = ok ? (z0 * ny + y0) * nx : 0;
+        rb[r] = ok ? cell[rw + xlo] : 0;
+        re[r] = ok ? cell[rw + xhi + 1] : 0;
     }
 }
 
@@ -1448,8 +1407,15 @@ struct PopArgs {
     int ccap;            // cells per grid of this run (<= kPopCellCap; pop_sort_cells)
     float* gp;           // (B, 8) grid lo[3], inv[3]
     int* gn;             // (B, 8) grid nb[3]
-    uint32_t* bent;      // (B, nslice, bdmax, 64) bonds of a slot: partner slot | type << 16 | lower << 31
-    uint16_t* bdeg;      // (B, ldn)
+    // bonds of a slot, by buffer parity (as the state): partner slot | type << 16 | lower << 31
+    uint32_t* bentb[2];  // (B, nslice, bdmax, 64)
+    uint16_t* bdegb[2];  // (B, ldn)
+    // the slot order change of a list build (the sort writes both): new slot -> old slot,
+    // old slot -> new slot; the permute moves a slot's state and bonds by them, bond
+    // partners re-indexed old slot -> new slot (slot-space reads near the slot, instead
+    // of the atom-space adjacency rows, which lie scattered by atom id)
+    int* inv;            // (B, ldn)
+    int* remap;          // (B, ldn)
     int bdmax;
     int kq;              // list quads per slot (4 kq >= the Verlet-list capacity)
     int* flag[2];        // (B) list rebuild needed, by step parity (the force kernel clears the next step's)
@@ -1539,6 +1505,14 @@ __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float
     const uint32_t fl = A.cm.aflags[(size_t)s * A.cm.afs + a];
     const float r = A.cm.radii[a];
     const PopBuf& B = A.buf[0];
+    {  // the bonds in the identity slot order (parity 0): the sliced adjacency of prepare()
+        const int deg = A.cm.bonds.deg[(size_t)s * A.cm.natom + a];
+        const uint32_t* g = A.cm.bonds.ent + A.cm.bonds.base[s] +
+                            A.cm.bonds.soff[(size_t)s * (A.cm.nslice + 1) + (a >> 6)] + (a & 63);
+        uint32_t* d = A.bentb[0] + ((size_t)s * A.cm.nslice + (a >> 6)) * A.bdmax * 64 + (a & 63);
+        for (int e = 0; e < deg; ++e) d[(size_t)e * 64] = g[(size_t)e * 64];
+        A.bdegb[0][i] = (uint16_t)deg;
+    }
     B.pos[i] = make_float4(x[0], x[1], x[2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
     B.vel[i] = make_float4(0.f, 0.f, 0.f, __uint_as_float(fl));
     B.frc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1725,14 +1699,10 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
         float* gp = A.gp + (size_t)s * 8;
         int* gn = A.gn + (size_t)s * 8;
         int nbv[3];
-        for (;;) {  // (bricks: whole bricks must fit the cap too)
 #pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                nbv[d] = (int)floorf(ext[d] / cs);
-                if (nbv[d] < 1) nbv[d] = 1;
-            }
-            if (kBrick == 0 || pop_ncell(nbv) <= A.ccap) break;
-            cs *= 1.02f;
+        for (int d = 0; d < 3; ++d) {
+            nbv[d] = (int)floorf(ext[d] / cs);
+            if (nbv[d] < 1) nbv[d] = 1;
         }
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
@@ -1872,6 +1842,8 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
             for (int k = beg; k < end; ++k) r += get(k) < a ? 1 : 0;
             aidn[beg + r] = a;
             slotn[a] = beg + r;
+            A.remap[base + t + u * kPopSortNT] = beg + r;  // (old slot t + u * kPopSortNT)
+            A.inv[base + beg + r] = t + u * kPopSortNT;
         }
     } else {
         for (int c = t; c <= ncell; c += kPopSortNT) {  // deterministic order inside a cell
@@ -1887,10 +1859,14 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
             }
         }
         __syncthreads();
+        const int* slot_old = A.buf[p].slot + base;
         for (int i = t; i < N; i += kPopSortNT) {
             const int a = get(i);
             if (IDS_LDS) aidn[i] = a;
             slotn[a] = i;
+            const int o = slot_old[a];
+            A.remap[base + o] = i;
+            A.inv[base + i] = o;
         }
     }
     phase(4);  // ranks inside the cells, new slot order stored
@@ -1940,34 +1916,32 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     const size_t base = (size_t)s * A.cm.ldn, k = base + i;
     const int q = A.par[s], p = q ^ 1;
     const PopBuf &O = A.buf[p], &B = A.buf[q];
-    const int a = B.aid[k];
-    const size_t o = base + O.slot[base + a];
-    const float4 x = O.pos[o];
+    const int o = A.inv[k];  // the slot's old slot
+    const float4 x = O.pos[base + o];
     B.pos[k] = x;
-    B.vel[k] = O.vel[o];
+    B.vel[k] = O.vel[base + o];
     // (no force: the force kernel of this step rewrites every slot's before any read)
     A.xb[k] = make_float4(x.x, x.y, x.z, 0.f);
     if (A.two) A.xo[k] = make_float4(x.x, x.y, x.z, 0.f);
     if (!BONDS) return;
-    // the atom's bonds (sorted adjacency of prepare()) with partners as slots
+    // the old slot's bonds, partners re-indexed old slot -> new slot
     const int nsl = A.cm.nslice;
-    const int* co = A.coff + (size_t)s * (A.cm.natom + 1);
-    const int r0 = co[a], deg = co[a + 1] - r0;
-    const uint32_t* g = A.csr + A.cbase[s] + r0;
-    uint32_t* d = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
-    const int* sl = B.slot + base;
-    for (int e0 = 0; e0 < deg; e0 += 4) {  // 4 entries, then their 4 slots, in flight together
+    const int deg = A.bdegb[p][base + o];
+    const uint32_t* g = A.bentb[p] + ((size_t)s * nsl + (o >> 6)) * A.bdmax * 64 + (o & 63);
+    uint32_t* d = A.bentb[q] + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
+    const int* rm = A.remap + base;
+    for (int e0 = 0; e0 < deg; e0 += 4) {  // 4 entries, then their 4 new slots, in flight together
         uint32_t v[4];
         int t[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = g[min(e0 + u, deg - 1)];
+        for (int u = 0; u < 4; ++u) v[u] = g[(size_t)min(e0 + u, deg - 1) * 64];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) t[u] = sl[v[u] & 0xffffu];
+        for (int u = 0; u < 4; ++u) t[u] = rm[v[u] & 0xffffu];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if (e0 + u < deg) d[(size_t)(e0 + u) * 64] = (v[u] & 0xffff0000u) | (uint32_t)t[u];
     }
-    A.bdeg[k] = (uint16_t)deg;
+    A.bdegb[q][k] = (uint16_t)deg;
 }
 
 
@@ -2011,15 +1985,14 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
     uint16_t* lst = reinterpret_cast<uint16_t*>(row);
     const float cut2 = A.P.cut_list * A.P.cut_list;
     int k = 0;
-    // The 27 cells are 9 x-runs of slots (with bricks up to 18: a run straddling a
-    // brick edge is two).  All run bounds are loaded together, then each z-layer's
-    // runs a batch of kFillW slots per run at once (the rare longer run finishes in a
-    // loop): 4 dependent memory round trips per slot in place of one per run and batch.
+    // The 27 cells are 9 x-runs of slots.  All 18 run bounds are loaded together,
+    // then each z-layer's 3 runs a batch of kFillW slots per run at once (the rare
+    // longer run finishes in a loop): 4 dependent memory round trips per slot in
+    // place of one per run and per batch.
     int cx, cy, cz;
     pop_cell_xyz(p0.x, p0.y, p0.z, gp, gp + 3, gn, cx, cy, cz);
-    constexpr int NR = 9 * kRunsPerRow, RL = NR / 3;  // runs, runs per z-layer
-    constexpr int FW = kBrick ? 2 : kFillW;           // (loads in flight per layer: RL * FW)
-    int rb[NR], re[NR];
+    constexpr int RL = 3, FW = kFillW;  // runs per z-layer, slots per run and batch
+    int rb[9], re[9];
     pop_runs(cx, cy, cz, cell, gn, rb, re);
     const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
     auto test = [&](int j, const float3& p) {
@@ -2153,9 +2126,9 @@ __device__ __noinline__ float4 pop_walk_pairs(const float4* pos, const int* cell
     float fx = 0.0f, fy = 0.0f, fz = 0.0f;
     int cx, cy, cz;
     pop_cell_xyz(bx, by, bz, gp, gp + 3, gn, cx, cy, cz);
-    int rb[9 * kRunsPerRow], re[9 * kRunsPerRow];
+    int rb[9], re[9];
     pop_runs(cx, cy, cz, cell, gn, rb, re);
-    for (int r = 0; r < 9 * kRunsPerRow; ++r)
+    for (int r = 0; r < 9; ++r)
         for (int j = rb[r]; j < re[r]; ++j) {
             const float4 p = pos[j];
             const float dx = p0.x - p.x, dy = p0.y - p.y, dz = p0.z - p.z;
@@ -2183,7 +2156,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     constexpr int U = kPopPairBatch;  // list quads per batch
     const int nsl = A.cm.nslice;
     const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
-    uint32_t* g = A.bent + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
+    uint32_t* g = A.bentb[A.par[s]] + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
     const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
     const float4 p0 = pos[i];
@@ -2202,9 +2175,9 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         const int r0 = co[a_id];
         deg = co[a_id + 1] - r0;
         ga = A.csr + A.cbase[s] + r0;
-        A.bdeg[base + i] = (uint16_t)deg;
+        A.bdegb[A.par[s]][base + i] = (uint16_t)deg;
     } else {
-        deg = A.bdeg[base + i];
+        deg = A.bdegb[A.par[s]][base + i];
     }
 #if IGM_POP_PREFETCH
     // Latency: the slot's loads, its first list quad and first bond entries go out in
@@ -3459,8 +3432,12 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     V.cell = Q.cell + (size_t)s0 * kPopCells;
     V.gp = Q.gp + (size_t)s0 * 8;
     V.gn = Q.gn + (size_t)s0 * 8;
-    V.bent = Q.bent + (size_t)s0 * nsl * Q.bdmax * 64;
-    V.bdeg = Q.bdeg + o;
+    for (int b = 0; b < 2; ++b) {
+        V.bentb[b] = Q.bentb[b] + (size_t)s0 * nsl * Q.bdmax * 64;
+        V.bdegb[b] = Q.bdegb[b] + o;
+    }
+    V.inv = Q.inv + o;
+    V.remap = Q.remap + o;
     V.flag[0] = Q.flag[0] + s0;
     V.flag[1] = Q.flag[1] + s0;
     V.oflag[0] = Q.oflag[0] + s0;
@@ -3523,8 +3500,15 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     IGM_TRY(workspace(c, "pop_cell", sizeof(int) * (size_t)S * kPopCells, &pcell));
     IGM_TRY(workspace(c, "pop_gp", sizeof(float) * 8 * (size_t)S, &pgp));
     IGM_TRY(workspace(c, "pop_gn", sizeof(int) * 8 * (size_t)S, &pgn));
-    IGM_TRY(workspace(c, "pop_bent", sizeof(uint32_t) * SL * Q.bdmax, &pbent));
-    IGM_TRY(workspace(c, "pop_bdeg", sizeof(uint16_t) * SL, &pbdeg));
+    IGM_TRY(workspace(c, "pop_bent", sizeof(uint32_t) * SL * Q.bdmax * 2, &pbent));
+    IGM_TRY(workspace(c, "pop_bdeg", sizeof(uint16_t) * SL * 2, &pbdeg));
+    {
+        void *pinv, *prm;
+        IGM_TRY(workspace(c, "pop_inv", sizeof(int) * SL, &pinv));
+        IGM_TRY(workspace(c, "pop_remap", sizeof(int) * SL, &prm));
+        Q.inv = (int*)pinv;
+        Q.remap = (int*)prm;
+    }
     IGM_TRY(workspace(c, "pop_flag", sizeof(int) * 2 * (size_t)S, &pfl));
     IGM_TRY(workspace(c, "pop_flist", sizeof(int) * (size_t)S, &pfli));
     IGM_TRY(workspace(c, "pop_nflag", sizeof(int) * 2 * kPopMaxGroups, &pnf));
@@ -3564,8 +3548,10 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.cell = (int*)pcell;
     Q.gp = (float*)pgp;
     Q.gn = (int*)pgn;
-    Q.bent = (uint32_t*)pbent;
-    Q.bdeg = (uint16_t*)pbdeg;
+    Q.bentb[0] = (uint32_t*)pbent;
+    Q.bentb[1] = (uint32_t*)pbent + SL * Q.bdmax;
+    Q.bdegb[0] = (uint16_t*)pbdeg;
+    Q.bdegb[1] = (uint16_t*)pbdeg + SL;
     Q.flag[0] = (int*)pfl;
     Q.flag[1] = (int*)pfl + S;
     Q.flist = (int*)pfli;
@@ -3602,8 +3588,9 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
         Q.dofs = (const double*)pdof;
     }
-    // bond rows as CSR (per-structure offsets by a block scan, structure bases on the host)
-    {
+    // bond rows as CSR (per-structure offsets by a block scan, structure bases on the host):
+    // the fused engine re-indexes bonds from atom space; the permute remaps slot space
+    if (kPopFused) {
         void *pco, *pcb, *pcsr;
         IGM_TRY(workspace(c, "pop_coff", sizeof(int) * (size_t)S * (N + 1), &pco));
         hipLaunchKernelGGL(pop_csr_scan_kernel, dim3(S), dim3(1024), 0, c->stream, pr.cm.bonds.deg, N, (int*)pco);

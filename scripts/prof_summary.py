@@ -75,6 +75,30 @@ def pmc(db):
     return list(c.execute(q))
 
 
+def pmc_by_anneal(db):
+    """{counter: [bytes of the pop_* / anneal_kernel dispatches of anneal 1, 2, ...]}: the
+    dispatches in id order, a new anneal at each run of pop_load launches (the groups'
+    loads) or at each anneal_kernel launch, so a warmup anneal and a timed one are
+    reported apart (value in KB as rocprofv3 gives FETCH_SIZE / WRITE_SIZE)"""
+    c = sqlite3.connect(db)
+    rows = list(c.execute('select dispatch_id, kernel_name, counter_name, sum(value) from counters_collection '
+                          'group by dispatch_id, kernel_name, counter_name order by dispatch_id'))
+    out, k, prev_load, last_id = {}, -1, False, None
+    for did, name, cn, v in rows:
+        is_load = 'pop_load' in name
+        if did != last_id:
+            if (is_load and not prev_load) or 'anneal_kernel' in name:
+                k += 1
+            prev_load = is_load
+            last_id = did
+        if k >= 0 and ('pop_' in name or 'anneal_kernel' in name):
+            lst = out.setdefault(cn, [])
+            while len(lst) <= k:
+                lst.append(0.0)
+            lst[k] += v
+    return out
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     for db in glob.glob(os.path.join(src, 'kt', '*.db')):
@@ -121,6 +145,18 @@ def main(src, dst):
                                                                        dur))
     with open(os.path.join(dst, 'hbm_traffic.txt'), 'w') as f:
         f.write('\n'.join(out) + '\n')
+        per = {}
+        for sub in ('fetch', 'write'):
+            for db in glob.glob(os.path.join(src, sub, '*.db')):
+                for cn, v in pmc_by_anneal(db).items():
+                    per[cn] = v
+        if per:
+            f.write('# per anneal (pop_* or anneal_kernel dispatches between anneal starts), HBM bytes after the\n'
+                    '# gfx950 correction (FETCH_SIZE x 2): anneal 1 is the warmup launch of the bench run\n')
+            for cn, v in sorted(per.items()):
+                corr = 2.0 if cn == 'FETCH_SIZE' else 1.0
+                f.write('%-10s %s\n' % (cn, '  '.join('anneal %d: %.4g' % (k + 1, x * 1024 * corr)
+                                                     for k, x in enumerate(v))))
     for fn in ('bench.log', 'host.txt'):
         p = os.path.join(src, fn)
         if os.path.exists(p):

@@ -58,3 +58,29 @@ def expand_per_pair(nrows, dist, prob):
     """per-pair golden -> per-row dist/prob (rows of a pair share dist/prob)."""
     nrows = np.asarray(nrows, np.int64)
     return np.repeat(dist[nrows > 0], nrows[nrows > 0]), np.repeat(prob[nrows > 0], nrows[nrows > 0])
+
+
+@pytest.fixture
+def heartbeat(request):
+    """For a GPU test that runs minutes inside one native call (the fp64 oracle on a
+    full protocol): a thread appends a line every 30 s to gpurun_out/heartbeat.txt, so a
+    runner that takes minutes without output for a hang sees the test alive (pytest
+    captures the test's own stdout and stderr)."""
+    import threading
+    import time
+    d = os.path.join(os.environ.get('GRAFT_REPO_ROOT', ROOT), 'gpurun_out')
+    os.makedirs(d, exist_ok=True)
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(30.0):
+            with open(os.path.join(d, 'heartbeat.txt'), 'a') as fh:
+                fh.write('%s %s alive\n' % (time.strftime('%H:%M:%S'), request.node.name))
+                fh.flush()
+            sys.stderr.flush()
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()
+    th.join(timeout=5)

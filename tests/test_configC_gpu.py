@@ -12,6 +12,7 @@ C ABI on the MI355X:
     oracle (population statistics) and bitwise against its own rerun.
 """
 import json
+import os
 
 import numpy as np
 import pytest
@@ -24,6 +25,7 @@ from igm_amd import synthetic as syn
 from igm_amd._lib import pair_dtype
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope='module')
@@ -111,7 +113,7 @@ def test_gpu_200kb_protocol_matches_oracle_and_reruns_bitwise():
     assert np.all(io['temp'] < 1.0)
 
 
-def test_gpu_200kb_full_protocol_on_astep_bonds_matches_oracle():
+def test_gpu_200kb_full_protocol_on_astep_bonds_matches_oracle(heartbeat):
     """The bench's own workload, at FULL protocol (lammps.py:285-356: 4 stages + relax,
     47 008 MD steps, CG): a 200 kb population runs one warmup A/M iteration on the GPU
     (AMIteration: Hi-C A-step over the population, Hi-C selection, anneal + CG); from
@@ -160,12 +162,21 @@ def test_gpu_200kb_full_protocol_on_astep_bonds_matches_oracle():
     assert np.all(np.isfinite(xg)) and np.all(ig['final_energy'] < ig['einitial'])
     t0 = time.perf_counter()
     xo, io, _ = oracle.mstep_run(prm, x0.copy(), atoms.radii, atoms.flags, poly, ptr, sb, seeds, nthreads=16)
-    print('[oracle] config C full protocol: %d structures on 16 threads in %.1f s' % (n, time.perf_counter() - t0))
+    t_oracle = time.perf_counter() - t0
+    print('[oracle] config C full protocol: %d structures on 16 threads in %.1f s' % (n, t_oracle))
     so = MS.population_stats(io, xo, poly, ptr, sb, atoms.nbead)
     so['env'] = io['env_energy'][:, 0] / atoms.nbead
     sg = MS.population_stats(ig, xg, poly, ptr, sb, atoms.nbead)
     sg['env'] = ig['env_energy'][:, 0] / atoms.nbead
     ok, pv = MS.same_population(sg, so, keys=('pair', 'bond', 'env', 'total', 'viol_frac', 'temp'))
     print('[ks] p-values', pv)
+    rec = {'test': 'test_gpu_200kb_full_protocol_on_astep_bonds_matches_oracle', 'structures': n,
+           'oracle_threads': 16, 'oracle_s': t_oracle, 'ks_p': pv, 'hic_bonds_per_structure': float(ptr[-1]) / n,
+           'gpu_final_energy_per_bead_median': float(np.median(sg['total'])),
+           'oracle_final_energy_per_bead_median': float(np.median(so['total']))}
+    d = os.path.join(os.environ.get('GRAFT_REPO_ROOT', ROOT), 'gpurun_out')
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, 'configC_full_protocol.json'), 'w') as fh:
+        json.dump(rec, fh, indent=1)
     assert ok, pv
     assert np.all(ig['temp'] < 1.0) and np.all(io['temp'] < 1.0)

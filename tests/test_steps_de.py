@@ -297,7 +297,8 @@ def test_gpu_config_chain_with_hip_kernels(tmp_path, config):
         for k in ('assignment', 'selected', 'indptr'):
             assert np.array_equal(sh[k], so[k]), k
     assert np.all(np.isfinite(h['x1'])) and not np.array_equal(h['x0'], h['x1'])
-    assert set(h['summary']['byrestraint']) == set(o['summary']['byrestraint'])
+    keys = lambda kind: {k.replace(str(tmp_path / kind), '<dir>') for k in out[kind]['summary']['byrestraint']}
+    assert keys('hip') == keys('oracle')
     assert 0.0 <= h['cfg']['runtime']['violation_score'] < 0.5
 
 
