@@ -223,7 +223,7 @@ def cpu_baseline_c(args, it, inp, snap, warmup):
                      'iterations: same coordinates, Hi-C restraints and seeds), fp64 C restatement, one structure '
                      'per thread on %d threads (affinity %d CPUs, cgroup quota %s CPUs); demo protocol MD steps x%g: '
                      '%.1f s, CG alone %.1f s, extrapolated to the full protocol %.0f s per %d structures (a '
-                     'full-protocol measurement: profiles/r04_cpu_c/)' % (n, warmup, n, avail, quota, sc, t_sample,
+                     'full-protocol measurement of the same kind: profiles/r04_parity/configC_full_protocol.json)' % (n, warmup, n, avail, quota, sc, t_sample,
                                                                           t_cg, t_full, n))
     return out
 
@@ -294,14 +294,16 @@ def bench_config_c(args, dev, world, rank, local, backend='nccl'):
             dist.barrier(device_ids=[local]) if backend == 'nccl' else dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.c_warmup):
+    for w in range(args.c_warmup):
+        progress('config C (pop=%d) warmup %d/%d' % (total, w + 1, args.c_warmup))
         it.step()
     barrier()
     want_cpu = args.c_cpu_scale > 0 and world == 1 and rank == 0
     snap = it.snapshot() if want_cpu else None
     anneal_ms, bytes_launch, steps = [], [], []
     t0 = time.perf_counter()
-    for _ in range(args.c_steps):
+    for k in range(args.c_steps):
+        progress('config C (pop=%d) timed step %d/%d' % (total, k + 1, args.c_steps))
         steps.append(it.step())
         anneal_ms.append(it.ctx.kernel_ms('anneal'))
         bytes_launch.append(it.algorithmic_anneal_bytes())
@@ -311,6 +313,7 @@ def bench_config_c(args, dev, world, rank, local, backend='nccl'):
     score = it.violation_score()
     info = it.info_host()
     nrows, nbonds, S_local = int(it.nrows), it.nbonds, it.S_local
+    progress('config C CPU baseline')
     cpu = cpu_baseline_c(args, it, inp, snap, args.c_warmup) if want_cpu else None
     a_ms = float(np.mean(anneal_ms))
     achieved = float(np.mean(bytes_launch)) / (a_ms * 1e-3) / 1e9
@@ -438,8 +441,42 @@ def measured_issue(config):
         return json.load(fh).get(config)
 
 
+class Progress(object):
+    """A stderr line every 30 s with the phase the bench is in (the run is minutes long and
+    its one JSON line comes at the end; runners that take a silent process for a hung one
+    see it alive).  Never on stdout."""
+
+    def __init__(self, rank):
+        import threading
+        self.phase, self.t0, self.rank = 'start', time.time(), rank
+        self.stop = threading.Event()
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def _run(self):
+        while not self.stop.wait(30.0):
+            print('[bench rank %d] %.0f s: %s' % (self.rank, time.time() - self.t0, self.phase), file=sys.stderr,
+                  flush=True)
+
+    def set(self, phase):
+        self.phase = phase
+
+    def close(self):
+        self.stop.set()
+
+
+PROGRESS = None
+
+
+def progress(phase):
+    if PROGRESS is not None:
+        PROGRESS.set(phase)
+
+
 def main():
+    global PROGRESS
     args = parse()
+    PROGRESS = Progress(int(os.environ.get('RANK', '0')))
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -469,14 +506,16 @@ def main():
             dist.barrier(device_ids=[local]) if backend == 'nccl' else dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
+        progress('config %s warmup %d/%d' % (args.config, w + 1, args.warmup))
         it.step()
     barrier()
     want_cpu = args.cpu_sample != 0 and world == 1 and rank == 0
     snap = it.snapshot() if want_cpu else None  # the first timed step's input state
     anneal_ms, bytes_launch, astep_s, mstep_s = [], [], [], []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        progress('config %s timed step %d/%d' % (args.config, k + 1, args.steps))
         tm = it.step()
         anneal_ms.append(it.ctx.kernel_ms('anneal'))
         if os.environ.get('IGM_PROF'):  # tuning: the LDS anneal kernel's cycle profile (perturbs the timing)
@@ -493,10 +532,12 @@ def main():
     nrows, nbonds, S_local, npairs, npairs_total = int(it.nrows), it.nbonds, it.S_local, it.npairs, it.npairs_total
     de = cblock = astep_cpu = cpu = None
     if want_cpu:
+        progress('CPU baselines of config %s' % args.config)
         nth, _, _ = host_threads(args)
         astep_cpu = cpu_baseline_astep(args, it, nth, npairs=2000 * nth)
         cpu = cpu_baseline(args, it, inp, snap)
     if rank == 0 and world == 1 and not args.no_de:  # the N=1 line carries it; scaling runs stay lean
+        progress('configuration D/E A-steps')
         de = bench_asteps_de(args, it.ctx)
     del it, snap
     torch.cuda.empty_cache()
@@ -548,6 +589,7 @@ def main():
             'excludes': 'host pair enumeration (select_pairs) and file I/O: inputs resident in HBM',
         }
         print(json.dumps(line), flush=True)
+    PROGRESS.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -1387,10 +1387,17 @@ __device__ __forceinline__ void pop_runs(int cx, int cy, int cz, const int* cell
     }
 }
 
+// a packed f32 triple (12 bytes, 4-byte aligned: one dwordx3 access per lane; a wave's
+// 64 consecutive triples are 768 contiguous bytes) -- the per-slot state nobody gathers
+// (forces, build positions) carries no fourth word to stream
+struct __attribute__((aligned(4))) pop_f3 {
+    float x, y, z;
+};
+
 struct PopBuf {
     float4* pos;   // (B, ldn): x, y, z, w = radius (bead) or -(radius + 1)
     float4* vel;   // (B, ldn): vx, vy, vz, w = the atom flags (bit pattern)
-    float4* frc;   // (B, ldn)
+    pop_f3* frc;   // (B, ldn)
     int* aid;      // (B, ldn) atom id of a slot
     int* slot;     // (B, ldn) slot of an atom id
 };
@@ -1400,7 +1407,7 @@ struct PopArgs {
     DevParams P;
     PopBuf buf[2];
     int* par;            // (B) buffer holding the current slot order
-    float4* xb;          // (B, ldn) position of the slot at its list build
+    pop_f3* xb;          // (B, ldn) position of the slot at its list build
     uint2* nl;           // (B, nslice, kq, 64) Verlet list: quads of u16 slot ids, padded with the own slot
     uint16_t* nnb;       // (B, ldn) list length, or kNnbWalk
     int* cell;           // (B, kPopCells) first slot of every cell of the build grid
@@ -1515,11 +1522,11 @@ __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float
     }
     B.pos[i] = make_float4(x[0], x[1], x[2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
     B.vel[i] = make_float4(0.f, 0.f, 0.f, __uint_as_float(fl));
-    B.frc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    B.frc[i] = pop_f3{0.f, 0.f, 0.f};
     B.aid[i] = a;
     B.slot[i] = a;
     const float inf = __int_as_float(0x7f800000);
-    A.xb[i] = make_float4(inf, inf, inf, 0.f);
+    A.xb[i] = pop_f3{inf, inf, inf};
     if (A.two) A.xo[i] = make_float4(inf, inf, inf, 0.f);
 }
 
@@ -1574,9 +1581,9 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     const size_t k = (size_t)s * A.cm.ldn + (live ? i : 0);
     float4 p = B.pos[k];
     float4 v = B.vel[k];
-    const float4 f = B.frc[k];
-    const float4 b = A.xb[k];
-    const float4 bo = A.two ? A.xo[k] : b;
+    const pop_f3 f = B.frc[k];
+    const pop_f3 b = A.xb[k];
+    const float4 bo = A.two ? A.xo[k] : make_float4(b.x, b.y, b.z, 0.f);
     const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
     int moved = 0, moved_o = 0;
     float mm[6] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
@@ -1921,7 +1928,7 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     B.pos[k] = x;
     B.vel[k] = O.vel[base + o];
     // (no force: the force kernel of this step rewrites every slot's before any read)
-    A.xb[k] = make_float4(x.x, x.y, x.z, 0.f);
+    A.xb[k] = pop_f3{x.x, x.y, x.z};
     if (A.two) A.xo[k] = make_float4(x.x, x.y, x.z, 0.f);
     if (!BONDS) return;
     // the old slot's bonds, partners re-indexed old slot -> new slot
@@ -2071,7 +2078,7 @@ __global__ void __launch_bounds__(kPopBS) pop_refilter_kernel(PopArgs A) {
     const size_t base = (size_t)s * A.cm.ldn;
     const float4* pos = A.buf[A.par[s]].pos + base;
     const float4 p0 = pos[i];
-    A.xb[base + i] = make_float4(p0.x, p0.y, p0.z, 0.f);  // the inner build position
+    A.xb[base + i] = pop_f3{p0.x, p0.y, p0.z};  // the inner build position
     if (!(p0.w >= 0.0f)) {
         A.nnb[base + i] = 0;
         return;
@@ -2227,7 +2234,8 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         if (nn == kNnbWalk) {
             // the walk covers the cells around the position of the grid's build (with
             // two-level lists the outer build: the cells hold the slots of that build)
-            const float4 b = (A.two ? A.xo : A.xb)[base + i];
+            const float4 b = A.two ? A.xo[base + i]
+                                   : make_float4(A.xb[base + i].x, A.xb[base + i].y, A.xb[base + i].z, 0.f);
             const float4 f = pop_walk_pairs(pos, A.cell + (size_t)s * kPopCells, A.gp + (size_t)s * 8,
                                             A.gn + (size_t)s * 8, b.x, b.y, b.z, i, p0, evfpi);
             fx = f.x;
@@ -2385,7 +2393,7 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
         } else {
             pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz);
         }
-        B.frc[k] = make_float4(fx, fy, fz, 0.f);
+        B.frc[k] = pop_f3{fx, fy, fz};
         if (S.integrate && !(fl & IGM_ATOM_FIXED)) {
             // final_integrate for the temperature only: the kicked velocity is not stored
             // (the next integrate, or the run's finish, redoes the kick from v and f)
@@ -2417,7 +2425,7 @@ __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S
     const size_t k = (size_t)s * A.cm.ldn + i;
     float4 v = B.vel[k];
     if (S.rescale && !(__float_as_uint(v.w) & IGM_ATOM_FIXED)) {  // the last step's final_integrate
-        const float4 f = B.frc[k];
+        const pop_f3 f = B.frc[k];
         kick_limit(v.x, v.y, v.z, f.x, f.y, f.z, S.dtf, S.vlim, S.vlimsq);
     }
     v.x *= factor;
@@ -2434,7 +2442,7 @@ __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S
     vel[a * 3 + 1] = v.y;
     vel[a * 3 + 2] = v.z;
     if (forces_out) {
-        const float4 f = B.frc[k];
+        const pop_f3 f = B.frc[k];
         forces_out[a * 3] = f.x;
         forces_out[a * 3 + 1] = f.y;
         forces_out[a * 3 + 2] = f.z;
@@ -3484,16 +3492,16 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         char nm[5][16];
         const char* what[5] = {"pos", "vel", "frc", "aid", "slot"};
         void* p[5];
-        const size_t sz[5] = {sizeof(float4), sizeof(float4), sizeof(float4), sizeof(int), sizeof(int)};
+        const size_t sz[5] = {sizeof(float4), sizeof(float4), sizeof(pop_f3), sizeof(int), sizeof(int)};
         for (int k = 0; k < 5; ++k) {
             snprintf(nm[k], sizeof(nm[k]), "pop_%s%d", what[k], b);
             IGM_TRY(workspace(c, nm[k], sz[k] * SL, &p[k]));
         }
-        Q.buf[b] = PopBuf{(float4*)p[0], (float4*)p[1], (float4*)p[2], (int*)p[3], (int*)p[4]};
+        Q.buf[b] = PopBuf{(float4*)p[0], (float4*)p[1], (pop_f3*)p[2], (int*)p[3], (int*)p[4]};
     }
     void *ppar, *pxb, *pnl, *pnnb, *pcell, *pgp, *pgn, *pbent, *pbdeg, *pfl, *pfli, *pnf, *pke, *pbb;
     IGM_TRY(workspace(c, "pop_par", sizeof(int) * S, &ppar));
-    IGM_TRY(workspace(c, "pop_xb", sizeof(float4) * SL, &pxb));
+    IGM_TRY(workspace(c, "pop_xb", sizeof(pop_f3) * SL, &pxb));
     Q.kq = (std::min(pr.cm.kcap, kPopListCap) + 3) / 4;
     IGM_TRY(workspace(c, "pop_nl", sizeof(uint2) * SL * Q.kq, &pnl));
     IGM_TRY(workspace(c, "pop_nnb", sizeof(uint16_t) * SL, &pnnb));
@@ -3542,7 +3550,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         }
     }
     Q.par = (int*)ppar;
-    Q.xb = (float4*)pxb;
+    Q.xb = (pop_f3*)pxb;
     Q.nl = (uint2*)pnl;
     Q.nnb = (uint16_t*)pnnb;
     Q.cell = (int*)pcell;
@@ -3841,14 +3849,21 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
     // config C -1.4 % against one 0.7 rmax skin for every run (scripts/gpu_skin_b.sh,
     // gpu_skin_seg.sh).  An explicit params.skin, or the IGM_SKIN_FACTOR tuning knob (one
     // skin for every run), is used for every run.
+    // The population engine (pr.big) pays more per list build and less per list entry, so
+    // its rule is longer at every temperature: 1.4 rmax at T0 = 5000, 1.15 at 500, 0.9 at
+    // 50, 0.475 at T0 <= 1 (measured at pop = 1000, protocol x0.05, same box: -4.8 % anneal
+    // against the LDS engine's rule; 1.2/1.0/0.8 -3.0 %, 1.6/1.3/1.0 -2.7 %,
+    // 1.8/1.5/1.2 +1.0 %; profiles/r04_ab/).
     const bool uniform_skin = prm->skin > 0 || getenv("IGM_SKIN_FACTOR") != nullptr;
     for (int k = 0; k < A.nseg; ++k) {
         if (uniform_skin) {
             A.seg_skin[k] = pr.P.skin;
         } else {
             const float rmax = 0.5f * (pr.P.cut_list - pr.P.skin);
-            const float f = 0.45f + 0.15f * log10f(fmaxf(A.seg_t0[k], 1.0f));
-            A.seg_skin[k] = fminf(fmaxf(f, 0.4f), 1.0f) * rmax;
+            const float lt = log10f(fmaxf(A.seg_t0[k], 1.0f));
+            const float f = pr.big ? fminf(fmaxf(0.475f + 0.25f * lt, 0.4f), 1.4f)
+                                   : fminf(fmaxf(0.45f + 0.15f * lt, 0.4f), 1.0f);
+            A.seg_skin[k] = f * rmax;
         }
     }
     if (const char* e = getenv("IGM_SKIN_SEG")) {

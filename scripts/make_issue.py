@@ -28,7 +28,7 @@ ent = {'bound': 'latency' if v.get('SQ_WAIT_ANY', 0.0) / max(v.get('SQ_WAVE_CYCL
        'unit': 'VALU pipe cycles per SIMD over the launch (2 cycles per wave64 VALU instruction)',
        'lds_bank_conflict_frac': v.get('SQ_LDS_BANK_CONFLICT', 0.0) / max(v.get('SQ_LDS_IDX_ACTIVE', 1.0), 1.0),
        'wait_frac': v.get('SQ_WAIT_ANY', 0.0) / max(v.get('SQ_WAVE_CYCLES', 1.0), 1.0),
-       'source': '%s/sq*.txt (rocprofv3 --pmc passes of bench.py --protocol-scale 0.05)' % d}
+       'source': '%s/sq*.txt (%s)' % (d, sys.argv[3] if len(sys.argv) > 3 else 'rocprofv3 --pmc passes')}
 path = 'bench_issue.json'
 cur = json.load(open(path)) if os.path.exists(path) else {}
 cur[config] = ent
