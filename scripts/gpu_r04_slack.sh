@@ -1,0 +1,14 @@
+#!/bin/bash
+# Slack-sorted Verlet lists: parity of the population engine, then A/B against IGM_POP_SLACK=0
+# (config C pop=1000 x0.05), twice each.
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/slack
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -p no:cacheprovider \
+  tests/test_mstep_paths_gpu.py tests/test_configC_gpu.py -k "not full_protocol and not actdist" \
+  > gpurun_out/slack/tests.log 2>&1
+rc=$?; tail -4 gpurun_out/slack/tests.log; [ $rc -eq 0 ] || exit $rc
+L=igm_amd/lib/ab
+TAG=slack ARGS="--config C --nstruct 1000 --protocol-scale 0.05" VARIANTS="IGM_POP_GROUPS=2
+IGM_HIP_LIB=$L/libigmhip_slk0.so
+IGM_POP_GROUPS=2
+IGM_HIP_LIB=$L/libigmhip_slk0.so" bash scripts/gpu_variants.sh
