@@ -1320,15 +1320,22 @@ constexpr int kPopMaxGroups = 64;  // structure groups (streams) of one run: bui
 constexpr int kPopCellCap = IGM_POP_CELL_CAP;
 constexpr int kPopCells = kPopCellCap + 2;  // cell offsets of a structure: real cells, non-bead run, end
 #ifndef IGM_POP_FILL_W
-#define IGM_POP_FILL_W 4
+#define IGM_POP_FILL_W 2
 #endif
 constexpr int kFillW = IGM_POP_FILL_W;  // list build: slots per x-run loaded in one batch
+#ifndef IGM_POP_FILL_TAIL
+#define IGM_POP_FILL_TAIL 4
+#endif
+constexpr int kFillTail = IGM_POP_FILL_TAIL;  // list build: slots past the batch loaded at a time
 #ifndef IGM_POP_LIST_CAP
 #define IGM_POP_LIST_CAP 48  // measured on config C: 48 beats 64 (fill occupancy) and 40 (more cell walks)
 #endif
 constexpr int kPopListCap = IGM_POP_LIST_CAP;  // Verlet-list entries per slot (more: the cell walk)
 #ifndef IGM_POP_PREFETCH
 #define IGM_POP_PREFETCH 1  // force kernel: software-pipelined list quads, bond entries with the slot's loads
+#endif
+#ifndef IGM_POP_QDEPTH
+#define IGM_POP_QDEPTH 2  // list quads in flight ahead of the one being gathered (2: -0.7 %, profiles/r04_ab)
 #endif
 #ifndef IGM_POP_FUSED
 // 1: list build + bond re-index inside the force kernel of a rebuild step.  Measured
@@ -1394,12 +1401,44 @@ struct __attribute__((aligned(4))) pop_f3 {
     float x, y, z;
 };
 
+// loads of the per-slot streams the force kernel reads once per step (list quads, bond
+// entries, velocity, flags, lengths): IGM_POP_NT marks them non-temporal, so they do not
+// displace the neighbour positions the gathers re-read from L1/L2
+#ifndef IGM_POP_NT
+#define IGM_POP_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ T pop_stream(const T* p) {
+#if IGM_POP_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ uint2 pop_stream(const uint2* p) {
+#if IGM_POP_NT
+    const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ pop_f3 pop_stream(const pop_f3* p) {
+#if IGM_POP_NT
+    const float* f = reinterpret_cast<const float*>(p);
+    return pop_f3{__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1), __builtin_nontemporal_load(f + 2)};
+#else
+    return *p;
+#endif
+}
+
 struct PopBuf {
     float4* pos;   // (B, ldn): x, y, z, w = radius (bead) or -(radius + 1)
-    float4* vel;   // (B, ldn): vx, vy, vz, w = the atom flags (bit pattern)
+    pop_f3* vel;   // (B, ldn)
     pop_f3* frc;   // (B, ldn)
     int* aid;      // (B, ldn) atom id of a slot
     int* slot;     // (B, ldn) slot of an atom id
+    uint8_t* flg;  // (B, ldn) the atom flags (every IGM_ATOM_* bit is below 0x100)
 };
 
 struct PopArgs {
@@ -1521,7 +1560,8 @@ __global__ void __launch_bounds__(kPopBS) pop_load_kernel(PopArgs A, const float
         A.bdegb[0][i] = (uint16_t)deg;
     }
     B.pos[i] = make_float4(x[0], x[1], x[2], (fl & IGM_ATOM_BEAD) ? r : -(r + 1.0f));
-    B.vel[i] = make_float4(0.f, 0.f, 0.f, __uint_as_float(fl));
+    B.vel[i] = pop_f3{0.f, 0.f, 0.f};
+    B.flg[i] = (uint8_t)fl;
     B.frc[i] = pop_f3{0.f, 0.f, 0.f};
     B.aid[i] = a;
     B.slot[i] = a;
@@ -1538,8 +1578,7 @@ __global__ void __launch_bounds__(kPopBS) pop_setvel_kernel(PopArgs A, const flo
     const PopBuf& B = A.buf[A.par[s]];
     const size_t k = (size_t)s * A.cm.ldn + i;
     const float* v = vsrc + (size_t)s * sstride + (size_t)B.aid[k] * 3;
-    const float w = B.vel[k].w;  // the flags
-    B.vel[k] = (__float_as_uint(w) & IGM_ATOM_FIXED) ? make_float4(0.f, 0.f, 0.f, w) : make_float4(v[0], v[1], v[2], w);
+    B.vel[k] = (B.flg[k] & IGM_ATOM_FIXED) ? pop_f3{0.f, 0.f, 0.f} : pop_f3{v[0], v[1], v[2]};
 }
 
 struct PopStep {
@@ -1580,15 +1619,16 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     const bool live = i < A.cm.natom;
     const size_t k = (size_t)s * A.cm.ldn + (live ? i : 0);
     float4 p = B.pos[k];
-    float4 v = B.vel[k];
-    const pop_f3 f = B.frc[k];
-    const pop_f3 b = A.xb[k];
+    pop_f3 v = pop_stream2(B.vel + k);
+    const uint32_t fl = pop_stream2(B.flg + k);
+    const pop_f3 f = pop_stream2(B.frc + k);
+    const pop_f3 b = pop_stream2(A.xb + k);
     const float4 bo = A.two ? A.xo[k] : make_float4(b.x, b.y, b.z, 0.f);
     const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
     int moved = 0, moved_o = 0;
     float mm[6] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
     if (live) {
-        if (S.integrate && !(__float_as_uint(v.w) & IGM_ATOM_FIXED)) {
+        if (S.integrate && !(fl & IGM_ATOM_FIXED)) {
             // the final_integrate half-kick of the previous step: the force kernel only
             // stores the force (its kinetic-energy partial used the same kicked velocity),
             // so the kick is redone here, bit for bit, instead of storing v in between
@@ -1631,6 +1671,15 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
         for (int w = 1; w < kPopBS / 64; ++w) m = fmaxf(m, red[w * 6 + threadIdx.x]);
         A.bbp[((size_t)s * A.nbs + lb % A.nbs) * 6 + threadIdx.x] = m;
     }
+}
+// the integrate kernel's once-per-step streams (IGM_POP_NT >= 2)
+template <typename T>
+__device__ __forceinline__ T pop_stream2(const T* p) {
+#if IGM_POP_NT >= 2
+    return pop_stream(p);
+#else
+    return *p;
+#endif
 }
 
 // One workgroup per flagged structure: the cell grid of build_nlist (cells of side >=
@@ -1927,6 +1976,7 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     const float4 x = O.pos[base + o];
     B.pos[k] = x;
     B.vel[k] = O.vel[base + o];
+    B.flg[k] = O.flg[base + o];
     // (no force: the force kernel of this step rewrites every slot's before any read)
     A.xb[k] = pop_f3{x.x, x.y, x.z};
     if (A.two) A.xo[k] = make_float4(x.x, x.y, x.z, 0.f);
@@ -1993,9 +2043,9 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
     const float cut2 = A.P.cut_list * A.P.cut_list;
     int k = 0;
     // The 27 cells are 9 x-runs of slots.  All 18 run bounds are loaded together,
-    // then each z-layer's 3 runs a batch of kFillW slots per run at once (the rare
-    // longer run finishes in a loop): 4 dependent memory round trips per slot in
-    // place of one per run and per batch.
+    // then each z-layer's 3 runs a batch of kFillW slots per run at once, the rest of a
+    // longer run kFillTail slots at a time (the hot runs' lists reach 3.4 rmax: ~10
+    // candidates per run; one dependent load per candidate there was +2 % anneal).
     int cx, cy, cz;
     pop_cell_xyz(p0.x, p0.y, p0.z, gp, gp + 3, gn, cx, cy, cz);
     constexpr int RL = 3, FW = kFillW;  // runs per z-layer, slots per run and batch
@@ -2024,7 +2074,20 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
         for (int r = 0; r < RL; ++r) {
 #pragma unroll
             for (int u = 0; u < FW; ++u) test(jj[r][u], pp[r][u]);
-            for (int j = rb[RL * g + r] + FW; j < re[RL * g + r]; ++j) test(j, pop_ld3(rp, j));
+            // the rest of a longer run, kFillTail loads in flight at a time (the slot itself
+            // past the run's end: never listed)
+            const int e = re[RL * g + r];
+            for (int j0 = rb[RL * g + r] + FW; j0 < e; j0 += kFillTail) {
+                float3 pt[kFillTail];
+                int jt[kFillTail];
+#pragma unroll
+                for (int u = 0; u < kFillTail; ++u) {
+                    jt[u] = j0 + u < e ? j0 + u : i;
+                    pt[u] = pop_ld3(rp, jt[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kFillTail; ++u) test(jt[u], pt[u]);
+            }
         }
     }
     // the last quad padded with the slot itself: a zero-distance entry adds no force
@@ -2171,7 +2234,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     fx = fy = fz = 0.0f;
     const float evfpi = evf * 0.318309886183790671537767526745f;
     const bool rebuilt = lrow != nullptr;
-    const int nn = rebuilt ? (nn_built <= 4 * A.kq ? nn_built : kNnbWalk) : A.nnb[base + i];
+    const int nn = rebuilt ? (nn_built <= 4 * A.kq ? nn_built : kNnbWalk) : pop_stream(A.nnb + base + i);
     const int* sl = A.buf[A.par[s]].slot + base;
     int a_id = 0;
     const uint32_t* ga = nullptr;  // atom-space adjacency (rebuilt step)
@@ -2184,17 +2247,17 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         ga = A.csr + A.cbase[s] + r0;
         A.bdegb[A.par[s]][base + i] = (uint16_t)deg;
     } else {
-        deg = A.bdegb[A.par[s]][base + i];
+        deg = pop_stream(A.bdegb[A.par[s]] + base + i);
     }
 #if IGM_POP_PREFETCH
     // Latency: the slot's loads, its first list quad and first bond entries go out in
     // one memory round trip (their addresses depend on (s, i) only; slots past the
     // atom's own are clamped into the allocated region and never used).
     uint2 qnext = make_uint2(i * 0x10001u, i * 0x10001u);
-    if (!rebuilt) qnext = gl[0];
+    if (!rebuilt) qnext = pop_stream(gl);
     uint32_t et0[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) et0[u] = rebuilt ? 0u : g[(size_t)min(u, A.bdmax - 1) * 64];
+    for (int u = 0; u < 4; ++u) et0[u] = rebuilt ? 0u : pop_stream(g + (size_t)min(u, A.bdmax - 1) * 64);
 #endif
     // Two list entries per packed-f32 op.  With t = 1/(r rc) from ONE rsq,
     //   sin(pi r / rc) = sin_rev(r2 t / 2)   and   evf rc sin / (pi r) = evfpi rc2 t sin,
@@ -2245,10 +2308,20 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
             const int nq = (nn + 3) >> 2;
             auto pairs = [&](auto fetch) {
 #if IGM_POP_PREFETCH
-                // one quad at a time, the next quad's load in flight with this one's gathers
+                // one quad at a time, the next QD quads' loads in flight with this one's gathers
+                constexpr int QD = IGM_POP_QDEPTH;
+                uint2 qb[QD];
+                qb[0] = qnext;
+#pragma unroll
+                for (int d = 1; d < QD; ++d) {
+                    qb[d] = make_uint2(i * 0x10001u, i * 0x10001u);
+                    if (!rebuilt && nq > d) qb[d] = pop_stream(gl + (size_t)d * 64);
+                }
                 for (int q = 0; q < nq; ++q) {
-                    const uint2 e = rebuilt ? make_uint2(lrow[2 * q], lrow[2 * q + 1]) : qnext;
-                    if (!rebuilt && q + 1 < nq) qnext = gl[(size_t)(q + 1) * 64];
+                    const uint2 e = rebuilt ? make_uint2(lrow[2 * q], lrow[2 * q + 1]) : qb[0];
+#pragma unroll
+                    for (int d = 0; d + 1 < QD; ++d) qb[d] = qb[d + 1];
+                    if (!rebuilt && q + QD < nq) qb[QD - 1] = pop_stream(gl + (size_t)(q + QD) * 64);
                     const float4 a0 = fetch(e.x & 0xffffu), a1 = fetch(e.x >> 16), a2 = fetch(e.y & 0xffffu),
                                  a3 = fetch(e.y >> 16);
                     pair2(a0, a1);
@@ -2302,7 +2375,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
             } else
 #endif
 #pragma unroll
-            for (int u = 0; u < 4; ++u) et[u] = g[(size_t)min(k0 + u, deg - 1) * 64];
+            for (int u = 0; u < 4; ++u) et[u] = pop_stream(g + (size_t)min(k0 + u, deg - 1) * 64);
         }
         float4 pt[4];
         float2 ct[4];
@@ -2378,8 +2451,8 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
     const PopBuf& B = A.buf[A.par[s]];
     double ke = 0.0;
     if (i < A.cm.natom) {
-        float4 v = B.vel[k];
-        const uint32_t fl = __float_as_uint(v.w);
+        pop_f3 v = pop_stream(B.vel + k);
+        const uint32_t fl = pop_stream(B.flg + k);
         float fx, fy, fz;
         if (FUSED && rebuilt) {
             uint32_t* row = lrow + threadIdx.x * (kPopListRow / 2);
@@ -2423,8 +2496,8 @@ __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S
     if (i >= A.cm.natom) return;
     const PopBuf& B = A.buf[A.par[s]];
     const size_t k = (size_t)s * A.cm.ldn + i;
-    float4 v = B.vel[k];
-    if (S.rescale && !(__float_as_uint(v.w) & IGM_ATOM_FIXED)) {  // the last step's final_integrate
+    pop_f3 v = B.vel[k];
+    if (S.rescale && !(B.flg[k] & IGM_ATOM_FIXED)) {  // the last step's final_integrate
         const pop_f3 f = B.frc[k];
         kick_limit(v.x, v.y, v.z, f.x, f.y, f.z, S.dtf, S.vlim, S.vlimsq);
     }
@@ -3432,7 +3505,8 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     V.cm.bonds.ntype = Q.cm.bonds.ntype + s0;
     if (V.P.vsmap) V.P.vsmap = Q.P.vsmap + s0;
     for (int b = 0; b < 2; ++b)
-        V.buf[b] = PopBuf{Q.buf[b].pos + o, Q.buf[b].vel + o, Q.buf[b].frc + o, Q.buf[b].aid + o, Q.buf[b].slot + o};
+        V.buf[b] = PopBuf{Q.buf[b].pos + o, Q.buf[b].vel + o, Q.buf[b].frc + o, Q.buf[b].aid + o, Q.buf[b].slot + o,
+                        Q.buf[b].flg + o};
     V.par = Q.par + s0;
     V.xb = Q.xb + o;
     V.nl = Q.nl + (size_t)s0 * nsl * Q.kq * 64;
@@ -3489,15 +3563,15 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     if (dmax > 0xFFFF) return fail(c, IGM_E_UNSUPPORTED, "an atom has %d bonds", dmax);
     Q.bdmax = dmax > 0 ? dmax : 1;
     for (int b = 0; b < 2; ++b) {
-        char nm[5][16];
-        const char* what[5] = {"pos", "vel", "frc", "aid", "slot"};
-        void* p[5];
-        const size_t sz[5] = {sizeof(float4), sizeof(float4), sizeof(pop_f3), sizeof(int), sizeof(int)};
-        for (int k = 0; k < 5; ++k) {
+        char nm[6][16];
+        const char* what[6] = {"pos", "vel", "frc", "aid", "slot", "flg"};
+        void* p[6];
+        const size_t sz[6] = {sizeof(float4), sizeof(pop_f3), sizeof(pop_f3), sizeof(int), sizeof(int), 1};
+        for (int k = 0; k < 6; ++k) {
             snprintf(nm[k], sizeof(nm[k]), "pop_%s%d", what[k], b);
             IGM_TRY(workspace(c, nm[k], sz[k] * SL, &p[k]));
         }
-        Q.buf[b] = PopBuf{(float4*)p[0], (float4*)p[1], (pop_f3*)p[2], (int*)p[3], (int*)p[4]};
+        Q.buf[b] = PopBuf{(float4*)p[0], (pop_f3*)p[1], (pop_f3*)p[2], (int*)p[3], (int*)p[4], (uint8_t*)p[5]};
     }
     void *ppar, *pxb, *pnl, *pnnb, *pcell, *pgp, *pgn, *pbent, *pbdeg, *pfl, *pfli, *pnf, *pke, *pbb;
     IGM_TRY(workspace(c, "pop_par", sizeof(int) * S, &ppar));
