@@ -1401,37 +1401,6 @@ struct __attribute__((aligned(4))) pop_f3 {
     float x, y, z;
 };
 
-// loads of the per-slot streams the force kernel reads once per step (list quads, bond
-// entries, velocity, flags, lengths): IGM_POP_NT marks them non-temporal, so they do not
-// displace the neighbour positions the gathers re-read from L1/L2
-#ifndef IGM_POP_NT
-#define IGM_POP_NT 0
-#endif
-template <typename T>
-__device__ __forceinline__ T pop_stream(const T* p) {
-#if IGM_POP_NT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ uint2 pop_stream(const uint2* p) {
-#if IGM_POP_NT
-    const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
-    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ pop_f3 pop_stream(const pop_f3* p) {
-#if IGM_POP_NT
-    const float* f = reinterpret_cast<const float*>(p);
-    return pop_f3{__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1), __builtin_nontemporal_load(f + 2)};
-#else
-    return *p;
-#endif
-}
-
 struct PopBuf {
     float4* pos;   // (B, ldn): x, y, z, w = radius (bead) or -(radius + 1)
     pop_f3* vel;   // (B, ldn)
@@ -1619,10 +1588,10 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     const bool live = i < A.cm.natom;
     const size_t k = (size_t)s * A.cm.ldn + (live ? i : 0);
     float4 p = B.pos[k];
-    pop_f3 v = pop_stream2(B.vel + k);
-    const uint32_t fl = pop_stream2(B.flg + k);
-    const pop_f3 f = pop_stream2(B.frc + k);
-    const pop_f3 b = pop_stream2(A.xb + k);
+    pop_f3 v = B.vel[k];
+    const uint32_t fl = B.flg[k];
+    const pop_f3 f = B.frc[k];
+    const pop_f3 b = A.xb[k];
     const float4 bo = A.two ? A.xo[k] : make_float4(b.x, b.y, b.z, 0.f);
     const float factor = S.rescale ? pop_factor(A, S, s, &fac) : 1.0f;
     int moved = 0, moved_o = 0;
@@ -1671,15 +1640,6 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
         for (int w = 1; w < kPopBS / 64; ++w) m = fmaxf(m, red[w * 6 + threadIdx.x]);
         A.bbp[((size_t)s * A.nbs + lb % A.nbs) * 6 + threadIdx.x] = m;
     }
-}
-// the integrate kernel's once-per-step streams (IGM_POP_NT >= 2)
-template <typename T>
-__device__ __forceinline__ T pop_stream2(const T* p) {
-#if IGM_POP_NT >= 2
-    return pop_stream(p);
-#else
-    return *p;
-#endif
 }
 
 // One workgroup per flagged structure: the cell grid of build_nlist (cells of side >=
@@ -2234,7 +2194,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     fx = fy = fz = 0.0f;
     const float evfpi = evf * 0.318309886183790671537767526745f;
     const bool rebuilt = lrow != nullptr;
-    const int nn = rebuilt ? (nn_built <= 4 * A.kq ? nn_built : kNnbWalk) : pop_stream(A.nnb + base + i);
+    const int nn = rebuilt ? (nn_built <= 4 * A.kq ? nn_built : kNnbWalk) : A.nnb[base + i];
     const int* sl = A.buf[A.par[s]].slot + base;
     int a_id = 0;
     const uint32_t* ga = nullptr;  // atom-space adjacency (rebuilt step)
@@ -2247,17 +2207,17 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         ga = A.csr + A.cbase[s] + r0;
         A.bdegb[A.par[s]][base + i] = (uint16_t)deg;
     } else {
-        deg = pop_stream(A.bdegb[A.par[s]] + base + i);
+        deg = A.bdegb[A.par[s]][base + i];
     }
 #if IGM_POP_PREFETCH
     // Latency: the slot's loads, its first list quad and first bond entries go out in
     // one memory round trip (their addresses depend on (s, i) only; slots past the
     // atom's own are clamped into the allocated region and never used).
     uint2 qnext = make_uint2(i * 0x10001u, i * 0x10001u);
-    if (!rebuilt) qnext = pop_stream(gl);
+    if (!rebuilt) qnext = gl[0];
     uint32_t et0[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) et0[u] = rebuilt ? 0u : pop_stream(g + (size_t)min(u, A.bdmax - 1) * 64);
+    for (int u = 0; u < 4; ++u) et0[u] = rebuilt ? 0u : g[(size_t)min(u, A.bdmax - 1) * 64];
 #endif
     // Two list entries per packed-f32 op.  With t = 1/(r rc) from ONE rsq,
     //   sin(pi r / rc) = sin_rev(r2 t / 2)   and   evf rc sin / (pi r) = evfpi rc2 t sin,
@@ -2315,13 +2275,13 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 #pragma unroll
                 for (int d = 1; d < QD; ++d) {
                     qb[d] = make_uint2(i * 0x10001u, i * 0x10001u);
-                    if (!rebuilt && nq > d) qb[d] = pop_stream(gl + (size_t)d * 64);
+                    if (!rebuilt && nq > d) qb[d] = gl[(size_t)d * 64];
                 }
                 for (int q = 0; q < nq; ++q) {
                     const uint2 e = rebuilt ? make_uint2(lrow[2 * q], lrow[2 * q + 1]) : qb[0];
 #pragma unroll
                     for (int d = 0; d + 1 < QD; ++d) qb[d] = qb[d + 1];
-                    if (!rebuilt && q + QD < nq) qb[QD - 1] = pop_stream(gl + (size_t)(q + QD) * 64);
+                    if (!rebuilt && q + QD < nq) qb[QD - 1] = gl[(size_t)(q + QD) * 64];
                     const float4 a0 = fetch(e.x & 0xffffu), a1 = fetch(e.x >> 16), a2 = fetch(e.y & 0xffffu),
                                  a3 = fetch(e.y >> 16);
                     pair2(a0, a1);
@@ -2375,7 +2335,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
             } else
 #endif
 #pragma unroll
-            for (int u = 0; u < 4; ++u) et[u] = pop_stream(g + (size_t)min(k0 + u, deg - 1) * 64);
+            for (int u = 0; u < 4; ++u) et[u] = g[(size_t)min(k0 + u, deg - 1) * 64];
         }
         float4 pt[4];
         float2 ct[4];
@@ -2451,8 +2411,8 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
     const PopBuf& B = A.buf[A.par[s]];
     double ke = 0.0;
     if (i < A.cm.natom) {
-        pop_f3 v = pop_stream(B.vel + k);
-        const uint32_t fl = pop_stream(B.flg + k);
+        pop_f3 v = B.vel[k];
+        const uint32_t fl = B.flg[k];
         float fx, fy, fz;
         if (FUSED && rebuilt) {
             uint32_t* row = lrow + threadIdx.x * (kPopListRow / 2);
