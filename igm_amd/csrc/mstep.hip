@@ -1328,9 +1328,16 @@ constexpr int kFillW = IGM_POP_FILL_W;  // list build: slots per x-run loaded in
 #endif
 constexpr int kFillTail = IGM_POP_FILL_TAIL;  // list build: slots past the batch loaded at a time
 #ifndef IGM_POP_LIST_CAP
-#define IGM_POP_LIST_CAP 48  // measured on config C: 48 beats 64 (fill occupancy) and 40 (more cell walks)
+#define IGM_POP_LIST_CAP 256
 #endif
 constexpr int kPopListCap = IGM_POP_LIST_CAP;  // Verlet-list entries per slot (more: the cell walk)
+#ifndef IGM_POP_ROW_CAP
+#define IGM_POP_ROW_CAP 40
+#endif
+// entries of the list build's LDS row per thread: the list collects there and is stored a
+// block of quads at a time, so the list capacity is not bound by the row (the row sets
+// the fill kernel's occupancy: 48 entries, 6 workgroups per CU)
+constexpr int kPopRowCap = IGM_POP_ROW_CAP;
 #ifndef IGM_POP_PREFETCH
 #define IGM_POP_PREFETCH 1  // force kernel: software-pipelined list quads, bond entries with the slot's loads
 #endif
@@ -1349,7 +1356,7 @@ constexpr bool kPopFused = IGM_POP_FUSED != 0;
 #define IGM_POP_OUTER_CAP 80
 #endif
 constexpr int kPopOuterCap = IGM_POP_OUTER_CAP;  // outer-list entries per slot (two-level lists)
-constexpr int kPopListRow = kPopListCap + 2;  // u16 per LDS list row of the build (odd word stride)
+constexpr int kPopListRow = kPopRowCap + 2;  // u16 per LDS list row of the build (odd word stride)
 // index of cell (cx, cy, cz) in the slot order of a grid of nb[3] cells: x-fastest.
 // (Measured on config C, pop=1000: bricks of 2^3 or 4^3 cells -- 64 or 256 consecutive
 // slots a compact blob instead of a rod along x -- were 12 % and 13 % SLOWER)
@@ -1993,15 +2000,35 @@ __device__ __forceinline__ float4 pop_ld(__amdgpu_buffer_rsrc_t r, uint32_t j) {
 // thread's LDS row `row` (kPopListRow u16), padded to whole quads with the slot itself,
 // stored as quads to the global list and its length (or kNnbWalk) to nnb.  Returns
 // the number of entries (> kcap: the slot takes its pairs from the cell walk).
+//   FLUSH: the row (rowcap entries) is stored and emptied whenever it holds flush_at
+// entries, so the list may be longer than the row (the fused force kernel reads its
+// list from the row: no flush, the list capacity capped at the row's).
+template <bool FLUSH>
 __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T, int s, int i, size_t base,
-                                             const float4* pos, float4 p0, uint32_t* row) {
+                                             const float4* pos, float4 p0, uint32_t* row, int rowcap) {
     const float* gp = A.gp + (size_t)s * 8;
     const int* gn = A.gn + (size_t)s * 8;
     const int* cell = A.cell + (size_t)s * kPopCells;
-    const int kcap = 4 * T.kq;  // <= kPopListCap
+    const int kcap = FLUSH ? 4 * T.kq : min(4 * T.kq, rowcap & ~3);
     uint16_t* lst = reinterpret_cast<uint16_t*>(row);
+    uint64_t* out = reinterpret_cast<uint64_t*>(T.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * T.kq * 64 + (i & 63));
     const float cut2 = A.P.cut_list * A.P.cut_list;
-    int k = 0;
+    // k: entries found; kr: entries in the row; qo: quads stored.  A flush check follows
+    // every group of at most 8 tests, so the row never holds more than flush_at + 7.
+    static_assert(kFillW <= 8 && kFillTail <= 8, "a test group must fit the row's slack");
+    const int flush_at = (rowcap - 8) & ~3;
+    int k = 0, kr = 0, qo = 0;
+    auto flush = [&]() {
+        if (FLUSH && kr >= flush_at) {
+#pragma unroll 1
+            for (int q = 0; q < (flush_at >> 2); ++q)
+                out[(size_t)(qo + q) * 64] = ((uint64_t)row[2 * q + 1] << 32) | row[2 * q];
+            qo += flush_at >> 2;
+#pragma unroll 1
+            for (int e = flush_at; e < kr; ++e) lst[e - flush_at] = lst[e];
+            kr -= flush_at;
+        }
+    };
     // The 27 cells are 9 x-runs of slots.  All 18 run bounds are loaded together,
     // then each z-layer's 3 runs a batch of kFillW slots per run at once, the rest of a
     // longer run kFillTail slots at a time (the hot runs' lists reach 3.4 rmax: ~10
@@ -2015,7 +2042,7 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
     auto test = [&](int j, const float3& p) {
         const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
         const bool in = j != i && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
-        if (in && k < kcap) lst[k] = (uint16_t)j;
+        if (in && k < kcap) lst[kr++] = (uint16_t)j;
         k += in ? 1 : 0;
     };
 #pragma unroll
@@ -2034,6 +2061,7 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
         for (int r = 0; r < RL; ++r) {
 #pragma unroll
             for (int u = 0; u < FW; ++u) test(jj[r][u], pp[r][u]);
+            flush();
             // the rest of a longer run, kFillTail loads in flight at a time (the slot itself
             // past the run's end: never listed)
             const int e = re[RL * g + r];
@@ -2047,16 +2075,16 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
                 }
 #pragma unroll
                 for (int u = 0; u < kFillTail; ++u) test(jt[u], pt[u]);
+                flush();
             }
         }
     }
     // the last quad padded with the slot itself: a zero-distance entry adds no force
-    for (int kk = k; kk < kcap && (kk & 3); ++kk) lst[kk] = (uint16_t)i;
-    const int nlist = k <= kcap ? ((k + 3) & ~3) : 0;  // entries incl. the padding
-    if (nlist > 0) {
-        uint64_t* out = reinterpret_cast<uint64_t*>(T.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * T.kq * 64 + (i & 63));
+    if (k <= kcap) {
+        for (int kk = kr; kk & 3; ++kk) lst[kk] = (uint16_t)i;
 #pragma unroll 1
-        for (int q = 0; q < nlist >> 2; ++q) out[(size_t)q * 64] = ((uint64_t)row[2 * q + 1] << 32) | row[2 * q];
+        for (int q = 0; q < (kr + 3) >> 2; ++q)
+            out[(size_t)(qo + q) * 64] = ((uint64_t)row[2 * q + 1] << 32) | row[2 * q];
     }
     T.nnb[base + i] = (uint16_t)(k <= kcap ? k : kNnbWalk);
     return k;
@@ -2082,7 +2110,7 @@ __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
     const float4 p0 = pos[i];
     const PopList T = A.two ? PopList{A.nlo, A.nnbo, A.kqo} : PopList{A.nl, A.nnb, A.kq};
     if (p0.w >= 0.0f)
-        pop_fill_slot(A, T, s, i, base, pos, p0, lrow + t * (ROW / 2));
+        pop_fill_slot<true>(A, T, s, i, base, pos, p0, lrow + t * (ROW / 2), ROW - 2);
     else
         T.nnb[base + i] = 0;
 }
@@ -2113,7 +2141,7 @@ __global__ void __launch_bounds__(kPopBS) pop_refilter_kernel(PopArgs A) {
     }
     uint32_t* row = lrow + t * (kPopListRow / 2);
     uint16_t* lst = reinterpret_cast<uint16_t*>(row);
-    const int kcap = 4 * A.kq;
+    const int kcap = min(4 * A.kq, kPopRowCap & ~3);  // (the list collects in the LDS row)
     const float cut2 = A.cut_in * A.cut_in;
     const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
     const uint2* go = A.nlo + ((size_t)s * A.cm.nslice + (i >> 6)) * A.kqo * 64 + (i & 63);
@@ -2158,15 +2186,25 @@ __device__ __noinline__ float4 pop_walk_pairs(const float4* pos, const int* cell
     pop_cell_xyz(bx, by, bz, gp, gp + 3, gn, cx, cy, cz);
     int rb[9], re[9];
     pop_runs(cx, cy, cz, cell, gn, rb, re);
+    constexpr int W = 4;  // candidates in flight (the slot itself past a run's end: no force)
     for (int r = 0; r < 9; ++r)
-        for (int j = rb[r]; j < re[r]; ++j) {
-            const float4 p = pos[j];
-            const float dx = p0.x - p.x, dy = p0.y - p.y, dz = p0.z - p.z;
-            const float f = soft_pair_bf(dx * dx + dy * dy + dz * dz, p0.w + p.w, evfpi);
-            const float m = j != i ? f : 0.0f;
-            fx += m * dx;
-            fy += m * dy;
-            fz += m * dz;
+        for (int j0 = rb[r]; j0 < re[r]; j0 += W) {
+            float4 pw[W];
+            int jw[W];
+#pragma unroll
+            for (int u = 0; u < W; ++u) {
+                jw[u] = j0 + u < re[r] ? j0 + u : i;
+                pw[u] = pos[jw[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < W; ++u) {
+                const float dx = p0.x - pw[u].x, dy = p0.y - pw[u].y, dz = p0.z - pw[u].z;
+                const float f = soft_pair_bf(dx * dx + dy * dy + dz * dz, p0.w + pw[u].w, evfpi);
+                const float m = jw[u] != i ? f : 0.0f;
+                fx += m * dx;
+                fy += m * dy;
+                fz += m * dz;
+            }
         }
     return make_float4(fx, fy, fz, 0.0f);
 }
@@ -2194,7 +2232,8 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     fx = fy = fz = 0.0f;
     const float evfpi = evf * 0.318309886183790671537767526745f;
     const bool rebuilt = lrow != nullptr;
-    const int nn = rebuilt ? (nn_built <= 4 * A.kq ? nn_built : kNnbWalk) : A.nnb[base + i];
+    const int nn = rebuilt ? (nn_built <= min(4 * A.kq, (kPopListRow - 2) & ~3) ? nn_built : kNnbWalk)
+                           : A.nnb[base + i];
     const int* sl = A.buf[A.par[s]].slot + base;
     int a_id = 0;
     const uint32_t* ga = nullptr;  // atom-space adjacency (rebuilt step)
@@ -2419,7 +2458,8 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
             const float4 p0 = B.pos[k];
             int nb = 0;
             if (p0.w >= 0.0f)
-                nb = pop_fill_slot(A, PopList{A.nl, A.nnb, A.kq}, s, i, base, B.pos + base, p0, row);
+                nb = pop_fill_slot<false>(A, PopList{A.nl, A.nnb, A.kq}, s, i, base, B.pos + base, p0, row,
+                                          kPopListRow - 2);
             else
                 A.nnb[k] = 0;
             pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, row, nb);
@@ -3536,7 +3576,9 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     void *ppar, *pxb, *pnl, *pnnb, *pcell, *pgp, *pgn, *pbent, *pbdeg, *pfl, *pfli, *pnf, *pke, *pbb;
     IGM_TRY(workspace(c, "pop_par", sizeof(int) * S, &ppar));
     IGM_TRY(workspace(c, "pop_xb", sizeof(pop_f3) * SL, &pxb));
-    Q.kq = (std::min(pr.cm.kcap, kPopListCap) + 3) / 4;
+    // the list capacity: kPopListCap, or a smaller neigh_capacity given in the params (the
+    // default 64 is the LDS engine's budget)
+    Q.kq = ((pr.P.kcap == kNeighBudget ? kPopListCap : std::min(pr.P.kcap, kPopListCap)) + 3) / 4;
     IGM_TRY(workspace(c, "pop_nl", sizeof(uint2) * SL * Q.kq, &pnl));
     IGM_TRY(workspace(c, "pop_nnb", sizeof(uint16_t) * SL, &pnnb));
     IGM_TRY(workspace(c, "pop_cell", sizeof(int) * (size_t)S * kPopCells, &pcell));

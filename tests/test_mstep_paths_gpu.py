@@ -161,3 +161,21 @@ def test_gpu_200kb_md_segment_tracks_oracle(ms, model200):
     moved = np.abs(xo - x).max()
     assert moved > 1.0
     assert np.abs(xg - xo).max() < 1e-3 * max(1.0, moved)
+
+
+@pytest.mark.parametrize('scale', [0.6, 0.4])
+def test_gpu_200kb_dense_lists_forces_match_oracle(ms, model200, scale):
+    """A compressed 200 kb structure: Verlet lists far longer than the list build's LDS row
+    (40 entries, stored a block of quads at a time) and, at 0.4, past the list capacity
+    (256: those slots take the cell walk).  f32 MD forces against the fp64 oracle."""
+    from scipy.spatial import cKDTree
+    atoms, poly, prm, ptr, sb, x = model200
+    xc = x.copy()
+    xc[:, :atoms.nbead] *= scale
+    rmax = float(atoms.radii[:atoms.nbead].max())
+    counts = cKDTree(xc[0, :atoms.nbead]).query_ball_point(xc[0, :atoms.nbead], 2.7 * rmax, return_length=True)
+    assert counts.max() > 60  # the row is flushed
+    f32, _ = ms.forces(prm, xc, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2, f32=True)
+    fo, _ = oracle.mstep_forces(prm, xc, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2)
+    err = np.linalg.norm(f32 - fo, axis=2)
+    assert np.linalg.norm(err) <= 1e-5 * np.linalg.norm(np.linalg.norm(fo, axis=2))
