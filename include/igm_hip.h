@@ -280,7 +280,9 @@ typedef struct {
     double env_semiaxes[IGM_MAX_ENVELOPES][3];
     double env_k[IGM_MAX_ENVELOPES];
     int32_t neigh_capacity; /* HBM neighbour-list budget, mean entries per atom (0 = 64); atoms past
-                               the budget take their pair forces from a walk of the build-time cell grid */
+                               the budget take their pair forces from a walk of the build-time cell grid.
+                               The population engine (structures too large for LDS) lists up to 256
+                               entries per atom when this is 0 or 64, else min(this, 256) */
     int32_t flags;          /* IGM_MSTEP_* below                        */
     int32_t env_kind[IGM_MAX_ENVELOPES]; /* IGM_ENV_ELLIPSOID (0) or IGM_ENV_VOLUME (1)  */
 } igm_mstep_params;

@@ -179,3 +179,15 @@ def test_gpu_200kb_dense_lists_forces_match_oracle(ms, model200, scale):
     fo, _ = oracle.mstep_forces(prm, xc, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2)
     err = np.linalg.norm(f32 - fo, axis=2)
     assert np.linalg.norm(err) <= 1e-5 * np.linalg.norm(np.linalg.norm(fo, axis=2))
+
+
+def test_gpu_200kb_small_list_capacity_forces_match_oracle(ms, model200):
+    """neigh_capacity below most list lengths: the population engine's slots past it take
+    their pairs from the cell walk; forces unchanged against the fp64 oracle."""
+    atoms, poly, prm, ptr, sb, x = model200
+    prm16 = M.params_from_cfg({'optimization': {'optimizer_options': F.DEMO_PROTOCOL}}, [((5500.0,) * 3, 1.0)])
+    prm16.neigh_capacity = 8
+    f32, _ = ms.forces(prm16, x, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2, f32=True)
+    fo, _ = oracle.mstep_forces(prm, x, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2)
+    err = np.linalg.norm(f32 - fo, axis=2)
+    assert np.linalg.norm(err) <= 1e-5 * np.linalg.norm(np.linalg.norm(fo, axis=2))
