@@ -99,13 +99,14 @@ def gather_rows(rows_u8, nrows, itemsize, cap, group=None):
     dev = rows_u8.device
     cdev = torch.device('cpu') if host else dev
     cap = max(int(cap), 1)
-    buf = torch.zeros(cap * itemsize + 8, dtype=torch.uint8, device=cdev)
+    off = (cap * itemsize + 7) & ~7  # the count at an 8-byte-aligned offset (an int64 view needs it)
+    buf = torch.zeros(off + 8, dtype=torch.uint8, device=cdev)
     buf[:nrows * itemsize] = rows_u8[:nrows * itemsize].to(cdev)
-    buf[cap * itemsize:].view(torch.int64).fill_(int(nrows))
+    buf[off:].view(torch.int64).fill_(int(nrows))
     out = torch.empty(world * buf.numel(), dtype=torch.uint8, device=cdev)
     dist.all_gather_into_tensor(out, buf, group=group)
     out = out.view(world, -1)
-    allc = out[:, cap * itemsize:].contiguous().view(torch.int64).view(-1).tolist()  # the one host sync
+    allc = out[:, off:].contiguous().view(torch.int64).view(-1).tolist()  # the one host sync
     rows = torch.cat([out[r, :c * itemsize] for r, c in enumerate(allc)])
     return (rows.to(dev) if host else rows), sum(allc)
 

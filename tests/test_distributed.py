@@ -160,3 +160,32 @@ def test_two_rank_de_asteps_equal_single_rank(tmp_path):
     t = np.sort(np.random.default_rng(2).lognormal(7.5, 0.4, (len(probes), S)), axis=1).astype(np.float32)
     omin, _, _, _ = A.fish_radial(bm, pop['copy_ptr'], pop['copy_idx'], probes, t, t)
     assert got['fish'].tobytes() == omin.tobytes()
+
+
+def _rows_worker(rank, world, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        # 12-byte rows (the DamID layout) and a capacity whose byte size is not a multiple of 8:
+        # the count word of each buffer still sits at an aligned offset
+        itemsize, cap = 12, 7
+        n = 3 + 2 * rank
+        rows = (np.arange(n * itemsize, dtype=np.uint8) + 50 * rank).astype(np.uint8)
+        got, total = pipeline.gather_rows(torch.from_numpy(rows), n, itemsize, cap)
+        if rank == 0:
+            want = np.concatenate([(np.arange((3 + 2 * r) * itemsize, dtype=np.uint8) + 50 * r).astype(np.uint8)
+                                   for r in range(world)])
+            np.save(out, got.numpy())
+            assert total == sum(3 + 2 * r for r in range(world))
+            assert np.array_equal(got.numpy(), want)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_rows_unaligned_capacity(tmp_path):
+    """gather_rows with a row size and capacity whose product is not 8-byte aligned (12-byte
+    DamID rows, capacity 7): the ranks' rows in rank order and their total (world 2, gloo)."""
+    out = str(tmp_path / 'rows.npy')
+    mp.spawn(_rows_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert os.path.exists(out)
