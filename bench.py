@@ -65,6 +65,9 @@ def parse():
     ap.add_argument('--c-warmup', type=int, default=1, help='warmup A/M iterations of the config C block')
     ap.add_argument('--c-cpu-scale', type=float, default=0.02,
                     help='protocol scale of the config C CPU-baseline sample (0: skip it)')
+    ap.add_argument('--c-shard', type=int, default=125,
+                    help='N=1 only: structures of the per-GPU shard sub-block of config C (the north-star run '
+                         'splits pop=1000 over 8 GPUs: 125 per GPU; 0: skip)')
     a = ap.parse_args()
     if a.nstruct is None:
         a.nstruct = 1000 if a.config == 'B' else 125
@@ -350,6 +353,29 @@ def bench_config_c(args, dev, world, rank, local, backend='nccl'):
     return out
 
 
+def bench_shard(args, dev):
+    """The per-GPU share of the north-star run (BASELINE.json configs[2] at 8 GPUs: pop=1000
+    split 125 per GPU): one warmup and c_steps timed A/M iterations of a args.c_shard-structure
+    200 kb population on this GPU, full protocol.  Its M-step time is what each of the 8 GPUs
+    spends; the A-step there runs over all 1000 structures, 1/8 of the pairs per rank (7.6 ms
+    for all of them at N=1, the config C block's actdist_ms), so the A-step of this shard's own
+    population stands in for it."""
+    sa = argparse.Namespace(**vars(args))
+    sa.c_total, sa.c_cpu_scale, sa.c_warmup = args.c_shard, 0.0, 1
+    progress('config C shard of %d structures' % args.c_shard)
+    r = bench_config_c(sa, dev, 1, 0, 0)
+    b = r['breakdown']
+    return {'value': r['value'], 'unit': 'structures/s', 'nstruct': args.c_shard, 'steps': r['steps'],
+            'ms_per_step': r['ms_per_step'], 'anneal_ms': b['anneal_ms'], 'cg_ms': b['cg_ms'],
+            'astep_ms': b['astep_ms'], 'mstep_ms': b['mstep_ms'], 'mean_rebuilds': b['mean_rebuilds'],
+            'median_final_energy_per_bead': b['median_final_energy_per_bead'], 'roofline_frac': r['roofline']['frac'],
+            'projected_8gpu_structures_per_s': 8.0 * args.c_shard * 1000.0 / r['ms_per_step'],
+            'note': 'one GPU running the %d-structure shard each of 8 GPUs owns in the pop=1000 north-star run; '
+                    'the projection (8 x shard / A/M iteration time) leaves out the population all-gather and the '
+                    'A-step pair split over 8 ranks (ms-scale against the ~%.0f s M-step)'
+                    % (args.c_shard, b['mstep_ms'] / 1000.0)}
+
+
 def bench_asteps_de(args, ctx):
     """Configuration D/E A-steps at full population size (200 kb diploid, 1000
     structures, bead-major .hss layout resident in HBM), timed with HIP events around
@@ -543,6 +569,8 @@ def main():
     torch.cuda.empty_cache()
     if args.config == 'B' and not args.no_c:  # every rank: the 200 kb pop=c_total population, strong split
         cblock = bench_config_c(args, dev, world, rank, local, backend)
+        if world == 1 and args.c_shard > 0 and args.c_shard != args.c_total:
+            cblock['shard%d' % args.c_shard] = bench_shard(args, dev)
     ms_per_step = 1000.0 * dt / max(args.steps, 1)
     total = S_local * world
     value = total * args.steps / dt

@@ -1311,21 +1311,23 @@ constexpr int kPopBS = 256;
 constexpr int kPopSortNT = 1024;
 constexpr int kPopMaxGroups = 64;  // structure groups (streams) of one run: build counters nflag[g], nflag2[g]
 #ifndef IGM_POP_CELL_CAP
-#define IGM_POP_CELL_CAP 49152
+#define IGM_POP_CELL_CAP 32768
 #endif
 // cells of a structure's grid in the population engine: the sort keeps their u16 counts
-// and the structure's u16 atom ids in one CU's LDS (49 152 cells + 29 838 ids: 158 KB), so
-// the cold runs' short cut_list (0.45 rmax skin: 35^3 cells over a 200 kb nucleus) keeps
-// cells of side cut_list instead of enlarging them past it
+// and the structure's u16 atom ids in one CU's LDS (32 768 cells + 29 838 ids: 124 KB).
+// The cap trades the cold runs' cell size (0.475 rmax skin: ~39 000 cells of side cut_list
+// over a 200 kb nucleus; at 32 768 they grow ~6 % past cut_list) against the sort's LDS
+// footprint: at 124 KB a sort workgroup shares its CU with a fill workgroup of the other
+// structure group (21.5 KB), at 158 KB (cap 49 152) with nothing.  Measured on config C
+// (pop = 1000, protocol x0.05, two groups, same box, profiles/r05_ab): 49 152 5 451 / 5 456
+// ms anneal, 32 768 5 366 / 5 363 / 5 308 ms, 24 576 5 551 ms.  (Round 3, one group in
+// effect at protocol x0.1, had measured 49 152 0.8 % faster than 32 768.)
 constexpr int kPopCellCap = IGM_POP_CELL_CAP;
 constexpr int kPopCells = kPopCellCap + 2;  // cell offsets of a structure: real cells, non-bead run, end
 #ifndef IGM_POP_FILL_W
 #define IGM_POP_FILL_W 2
 #endif
 constexpr int kFillW = IGM_POP_FILL_W;  // list build: slots per x-run loaded in one batch
-#ifndef IGM_POP_TRIM
-#define IGM_POP_TRIM 1  // list build: the 27-cell walk trimmed to the cells within cut_list (pop_runs_trim)
-#endif
 #ifndef IGM_POP_FILL_TAIL
 #define IGM_POP_FILL_TAIL 4
 #endif
@@ -1404,41 +1406,6 @@ __device__ __forceinline__ void pop_runs(int cx, int cy, int cz, const int* cell
     }
 }
 
-// pop_runs trimmed to the cells a position p in cell (cx, cy, cz) can reach within cut
-// (cut2 = cut^2): a row (dy, dz) whose nearest face pair is cut away is empty, and its
-// x-run drops the cell on either end that the position's distance to the shared face,
-// with the row's y/z offsets, puts past cut.  For a position uniformly in its cell 12
-// edge cells are reachable with probability pi/4 and 8 corner cells with pi/6 (20.6 of 27
-// cells).  A trimmed cell holds no slot within cut of p (its face distance is a lower bound,
-// less a tolerance of 1e-3 of the cell side far above the binning's rounding), so the list
-// -- its entries and their order -- is that of the full walk.
-__device__ __forceinline__ void pop_runs_trim(const float4& p, int cx, int cy, int cz, const float* gp,
-                                              const int* cell, const int* nb, float cut2, int (&rb)[9],
-                                              int (&re)[9]) {
-    const int nx = nb[0], ny = nb[1], nz = nb[2];
-    const float pp[3] = {p.x, p.y, p.z};
-    const int cc[3] = {cx, cy, cz};
-    float glo[3], ghi[3];  // distances to the cell's lower and upper faces, less the tolerance
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const float side = 1.0f / gp[3 + d], off = (pp[d] - gp[d]) - (float)cc[d] * side, tol = 1.0e-3f * side;
-        glo[d] = fmaxf(off - tol, 0.0f);
-        ghi[d] = fmaxf(side - off - tol, 0.0f);
-    }
-    const float lo2 = glo[0] * glo[0], hi2 = ghi[0] * ghi[0];
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-        const int dz = r / 3 - 1, dy = r % 3 - 1, z0 = cz + dz, y0 = cy + dy;
-        const float gy = dy < 0 ? glo[1] : (dy > 0 ? ghi[1] : 0.0f), gz = dz < 0 ? glo[2] : (dz > 0 ? ghi[2] : 0.0f);
-        const float base = gy * gy + gz * gz;
-        const bool ok = z0 >= 0 && z0 < nz && y0 >= 0 && y0 < ny && base < cut2;
-        const int xlo = cx > 0 && lo2 + base < cut2 ? cx - 1 : cx, xhi = cx + 1 < nx && hi2 + base < cut2 ? cx + 1 : cx;
-        const int rw = ok ? (z0 * ny + y0) * nx : 0;
-        rb[r] = ok ? cell[rw + xlo] : 0;
-        re[r] = ok ? cell[rw + xhi + 1] : 0;
-    }
-}
-
 // a packed f32 triple (12 bytes, 4-byte aligned: one dwordx3 access per lane; a wave's
 // 64 consecutive triples are 768 contiguous bytes) -- the per-slot state nobody gathers
 // (forces, build positions) carries no fourth word to stream
@@ -1506,12 +1473,6 @@ struct PopArgs {
     int* flist2;         // (B) the structures whose inner list is rebuilt this step
     int* nflag2;         // (1)
     unsigned long long* sprof;  // optional (8): the sort kernel's phase cycles, summed (profiling)
-    // Block windows (pop_sort_kernel writes them, pop_wforce_kernel stages them): the slot intervals of every
-    // kPopBS-slot block, staged in LDS by the force kernel; list entries and bond partners
-    // are window indices (< kWinCap) or kWinCap + slot (outside the window)
-    int* win;            // (B, nbs, 8): lo[3], len[3]
-    uint32_t* bnt;       // (B, nslice, kb4, 64, 4) bonds: partner entry | type << 16 | lower << 31, 4 per lane-chunk
-    int kb4;             // bond chunks of 4 per slot (>= bdmax / 4)
 };
 
 // one Verlet list of the engine (the inner one, or the outer one of two-level lists)
@@ -1691,112 +1652,6 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
         for (int w = 1; w < kPopBS / 64; ++w) m = fmaxf(m, red[w * 6 + threadIdx.x]);
         A.bbp[((size_t)s * A.nbs + lb % A.nbs) * 6 + threadIdx.x] = m;
     }
-}
-
-#ifndef IGM_POP_WIN_DEFAULT
-#define IGM_POP_WIN_DEFAULT 0  // block windows off unless IGM_POP_WIN=1 (see kWinCap)
-#endif
-#ifndef IGM_POP_WIN_CAP
-#define IGM_POP_WIN_CAP 1400
-#endif
-// slots of a block's LDS window (16 B each: 22.4 KB, 7 force workgroups per CU).  Measured on
-// config C (pop = 1000, the bench's timed iteration, IGM_POP_STATS): the three intervals of a
-// 256-slot block hold 975-1180 slots on average, at most 2 324 (hot run); 19 % of the hot run's
-// blocks and 1.3 % of the T0 = 500 run's need more than 1 536 (a clipped window: the entries
-// outside it are read from HBM).  Cap 2 040 (5 workgroups per CU): force kernel 1 644 us per
-// step against 1 560 for the plain gathers; cap 1 400 at 7 waves per SIMD: 1 316 us
-// (profiles/r05_ab).
-constexpr int kWinCap = IGM_POP_WIN_CAP;
-
-// The slot window of a block of kPopBS slots (the slots its atoms' neighbours can be in):
-// in the slot order of the build (cells x-fastest), the 27 cells around any cell c of the
-// block's cells [c0, c1] lie in the three cell ranges [c0 + dz L - R - 1, c1 + dz L + R + 1]
-// (dz = -1, 0, 1; L cells per layer, R per row), i.e. in three slot intervals.  They are
-// staged in LDS back to back (interval k at the offset of the ones before it), so a
-// neighbour's position is one LDS read instead of one L1 tag lookup.  Past `cap` slots the
-// row margin m shrinks (rows y +- 1 partly covered; entries outside are read from HBM).
-struct PopWin {
-    int lo[3];   // first slot of each interval (merged, ascending)
-    int len[3];  // slots (0: unused)
-};
-
-__device__ __forceinline__ int pop_win_index(const PopWin& W, int j) {
-    int off = 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const unsigned d = (unsigned)(j - W.lo[k]);
-        if (d < (unsigned)W.len[k]) return off + (int)d;
-        off += W.len[k];
-    }
-    return -1;
-}
-
-// window entry of slot j: its index in the block's window, or kWinCap + j outside it
-__device__ __forceinline__ uint32_t pop_win_enc(const PopWin& W, int j) {
-    const int w = pop_win_index(W, j);
-    return (uint32_t)(w >= 0 ? w : kWinCap + j);
-}
-
-// the slot of window index k (k < the window's total)
-__device__ __forceinline__ int pop_win_slot(const PopWin& W, int k) {
-    return k < W.len[0] ? W.lo[0] + k : (k < W.len[0] + W.len[1] ? W.lo[1] + k - W.len[0]
-                                                                  : W.lo[2] + k - W.len[0] - W.len[1]);
-}
-
-// the window of the block whose bead slots run to s1 and lie in cells [c0, c1] of a grid of
-// nx * ny * (ncell / (nx ny)) cells; off(c) = the first slot of cell c
-template <typename Off>
-__device__ inline PopWin pop_window_core(Off off, int nx, int ny, int ncell, int c0, int c1, int s1, int cap) {
-    const int L = nx * ny;
-    int lo[3], hi[3];
-    auto build = [&](int m) {  // the merged slot intervals for row margin m; returns their total
-        int n = 0, tot = 0;
-        for (int dz = -1; dz <= 1; ++dz) {
-            int a = c0 + dz * L - m, z = c1 + dz * L + m;
-            a = a < 0 ? 0 : a;
-            z = z > ncell - 1 ? ncell - 1 : z;
-            if (a > z) continue;
-            const int sa = off(a), sz = off(z + 1);
-            if (sz <= sa) continue;
-            if (n > 0 && sa <= hi[n - 1]) {
-                hi[n - 1] = max(hi[n - 1], sz);
-            } else {
-                lo[n] = sa;
-                hi[n] = sz;
-                ++n;
-            }
-        }
-        for (int k = 0; k < n; ++k) tot += hi[k] - lo[k];
-        for (int k = n; k < 3; ++k) lo[k] = hi[k] = 0;
-        return tot;
-    };
-    const int m = nx + 1;
-    if (build(m) > cap) {  // the largest margin that fits
-        int good = -1, l = 0, h = m - 1;
-        while (l <= h) {
-            const int mid = (l + h) >> 1;
-            if (build(mid) <= cap) {
-                good = mid;
-                l = mid + 1;
-            } else {
-                h = mid - 1;
-            }
-        }
-        if (good >= 0) {
-            build(good);
-        } else {  // denser than cap even without margins: the block's own cells, clipped around it
-            lo[0] = max(off(c0), s1 + 1 - cap);
-            hi[0] = min(off(c1 + 1), lo[0] + cap);
-            lo[1] = hi[1] = lo[2] = hi[2] = 0;
-        }
-    }
-    PopWin W;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        W.lo[k] = lo[k];
-        W.len[k] = hi[k] - lo[k];
-    }
-    return W;
 }
 
 // One workgroup per flagged structure: the cell grid of build_nlist (cells of side >=
@@ -2045,32 +1900,6 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
     phase(4);  // ranks inside the cells, new slot order stored
     int* cg = A.cell + (size_t)s * kPopCells;
     for (int c = t; c <= ncell + 1; c += kPopSortNT) cg[c] = off(c);
-    if (A.win && t < A.nbs) {  // the windows of the structure's blocks, from the offsets in LDS
-        PopWin W;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) W.lo[k] = W.len[k] = 0;
-        const int nbead = off(ncell), s0 = t * kPopBS, s1 = min(s0 + kPopBS, nbead) - 1;
-        if (s0 <= s1) {
-            auto cell_of = [&](int x) {  // the cell holding slot x: the last cell starting at or before it
-                int l = 0, h = ncell - 1;
-                while (l < h) {
-                    const int mid = (l + h + 1) >> 1;
-                    if (off(mid) <= x)
-                        l = mid;
-                    else
-                        h = mid - 1;
-                }
-                return l;
-            };
-            W = pop_window_core(off, nb[0], nb[1], ncell, cell_of(s0), cell_of(s1), s1, kWinCap);
-        }
-        int* wo = A.win + ((size_t)s * A.nbs + t) * 8;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            wo[k] = W.lo[k];
-            wo[3 + k] = W.len[k];
-        }
-    }
     if (t == 0) A.par[s] = q;
 #if IGM_POP_SORT_PROF
     if (A.sprof) {
@@ -2130,19 +1959,6 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
     const uint32_t* g = A.bentb[p] + ((size_t)s * nsl + (o >> 6)) * A.bdmax * 64 + (o & 63);
     uint32_t* d = A.bentb[q] + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const int* rm = A.remap + base;
-    // block windows: the bonds also in window form (pop_wforce_kernel), 4 per 16-byte
-    // lane-chunk, the last chunk padded with the slot itself (a zero-distance bond adds nothing)
-    PopWin W;
-    uint4* wo = nullptr;
-    if (A.win) {
-        const int* wp = A.win + ((size_t)s * A.nbs + i / kPopBS) * 8;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            W.lo[k] = wp[k];
-            W.len[k] = wp[3 + k];
-        }
-        wo = reinterpret_cast<uint4*>(A.bnt) + ((size_t)s * nsl + (i >> 6)) * A.kb4 * 64 + (i & 63);
-    }
     for (int e0 = 0; e0 < deg; e0 += 4) {  // 4 entries, then their 4 new slots, in flight together
         uint32_t v[4];
         int t[4];
@@ -2153,13 +1969,6 @@ __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if (e0 + u < deg) d[(size_t)(e0 + u) * 64] = (v[u] & 0xffff0000u) | (uint32_t)t[u];
-        if (wo) {
-            const uint32_t self = pop_win_enc(W, i);
-            uint32_t w4[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) w4[u] = e0 + u < deg ? (v[u] & 0xffff0000u) | pop_win_enc(W, t[u]) : self;
-            wo[(size_t)(e0 >> 2) * 64] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-        }
     }
     A.bdegb[q][k] = (uint16_t)deg;
 }
@@ -2185,26 +1994,6 @@ __device__ __forceinline__ float4 pop_ld(__amdgpu_buffer_rsrc_t r, uint32_t j) {
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 
-// the window of block b of structure s from the stored grid (diagnostics; the sort
-// kernel computes the engine's windows from its LDS cell offsets)
-__device__ inline PopWin pop_block_window(const PopArgs& A, int s, int b, int cap) {
-    PopWin W;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) W.lo[k] = W.len[k] = 0;
-    const int* cell = A.cell + (size_t)s * kPopCells;
-    const int* gn = A.gn + (size_t)s * 8;
-    const float* gp = A.gp + (size_t)s * 8;
-    const int nx = gn[0], ny = gn[1], ncell = nx * gn[2] * ny;
-    const int nbead = cell[ncell];  // the non-bead run starts after the last cell
-    const int s0 = b * kPopBS, s1 = min(s0 + kPopBS, nbead) - 1;
-    if (s0 > s1) return W;
-    const size_t base = (size_t)s * A.cm.ldn;
-    const pop_f3 x0 = A.xb[base + s0], x1 = A.xb[base + s1];
-    const int c0 = pop_cell_index(x0.x, x0.y, x0.z, gp, gp + 3, gn);
-    const int c1 = pop_cell_index(x1.x, x1.y, x1.z, gp, gp + 3, gn);
-    return pop_window_core([&](int c) { return cell[c]; }, nx, ny, ncell, c0, c1, s1, cap);
-}
-
 // Verlet list of every bead slot of a flagged structure: the 27 cells around its cell,
 // each x-run of cells one contiguous slot range.  Measured on config C (kernel traces,
 // scripts/gpu_profab.sh): collecting the list in an LDS row and storing it a quad at a
@@ -2219,11 +2008,9 @@ __device__ inline PopWin pop_block_window(const PopArgs& A, int s, int b, int ca
 //   FLUSH: the row (rowcap entries) is stored and emptied whenever it holds flush_at
 // entries, so the list may be longer than the row (the fused force kernel reads its
 // list from the row: no flush, the list capacity capped at the row's).
-//   ENC: the entries in window form (pop_win_enc with the block's window W: pop_wforce_kernel).
-template <bool FLUSH, bool ENC = false>
+template <bool FLUSH>
 __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T, int s, int i, size_t base,
-                                             const float4* pos, float4 p0, uint32_t* row, int rowcap,
-                                             const PopWin* W = nullptr) {
+                                             const float4* pos, float4 p0, uint32_t* row, int rowcap) {
     const float* gp = A.gp + (size_t)s * 8;
     const int* gn = A.gn + (size_t)s * 8;
     const int* cell = A.cell + (size_t)s * kPopCells;
@@ -2255,32 +2042,12 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
     pop_cell_xyz(p0.x, p0.y, p0.z, gp, gp + 3, gn, cx, cy, cz);
     constexpr int RL = 3, FW = kFillW;  // runs per z-layer, slots per run and batch
     int rb[9], re[9];
-#if IGM_POP_TRIM
-    pop_runs_trim(p0, cx, cy, cz, gp, cell, gn, cut2, rb, re);
-#else
     pop_runs(cx, cy, cz, cell, gn, rb, re);
-#endif
     const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
-    // ENC: a run inside one window interval encodes by one add (its delta); a run the window
-    // does not hold whole (a clipped window) takes pop_win_enc per entry
-    constexpr int kSlow = -0x40000000;
-    int dl[9];
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-        dl[r] = kSlow;
-        if (ENC) {
-            int off = 0;
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                if (rb[r] >= W->lo[q] && re[r] <= W->lo[q] + W->len[q]) dl[r] = off - W->lo[q];
-                off += W->len[q];
-            }
-        }
-    }
-    auto test = [&](int j, const float3& p, int d) {
+    auto test = [&](int j, const float3& p) {
         const float ddx = p0.x - p.x, ddy = p0.y - p.y, ddz = p0.z - p.z;
         const bool in = j != i && ddx * ddx + ddy * ddy + ddz * ddz < cut2;
-        if (in && k < kcap) lst[kr++] = (uint16_t)(!ENC ? (uint32_t)j : d != kSlow ? (uint32_t)(j + d) : pop_win_enc(*W, j));
+        if (in && k < kcap) lst[kr++] = (uint16_t)j;
         k += in ? 1 : 0;
     };
 #pragma unroll
@@ -2298,7 +2065,7 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
 #pragma unroll
         for (int r = 0; r < RL; ++r) {
 #pragma unroll
-            for (int u = 0; u < FW; ++u) test(jj[r][u], pp[r][u], dl[RL * g + r]);
+            for (int u = 0; u < FW; ++u) test(jj[r][u], pp[r][u]);
             flush();
             // the rest of a longer run, kFillTail loads in flight at a time (the slot itself
             // past the run's end: never listed)
@@ -2312,15 +2079,14 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
                     pt[u] = pop_ld3(rp, jt[u]);
                 }
 #pragma unroll
-                for (int u = 0; u < kFillTail; ++u) test(jt[u], pt[u], dl[RL * g + r]);
+                for (int u = 0; u < kFillTail; ++u) test(jt[u], pt[u]);
                 flush();
             }
         }
     }
     // the last quad padded with the slot itself: a zero-distance entry adds no force
     if (k <= kcap) {
-        const uint16_t self = (uint16_t)(ENC ? pop_win_enc(*W, i) : (uint32_t)i);
-        for (int kk = kr; kk & 3; ++kk) lst[kk] = self;
+        for (int kk = kr; kk & 3; ++kk) lst[kk] = (uint16_t)i;
 #pragma unroll 1
         for (int q = 0; q < (kr + 3) >> 2; ++q)
             out[(size_t)(qo + q) * 64] = ((uint64_t)row[2 * q + 1] << 32) | row[2 * q];
@@ -2348,24 +2114,11 @@ __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
     const float4* pos = A.buf[A.par[s]].pos + base;
     const float4 p0 = pos[i];
     const PopList T = A.two ? PopList{A.nlo, A.nnbo, A.kqo} : PopList{A.nl, A.nnb, A.kq};
-    if (p0.w >= 0.0f) {
-        if (A.win) {  // block windows: entries in window form
-            const int* wp = A.win + ((size_t)s * A.nbs + blk) * 8;
-            PopWin W;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                W.lo[k] = wp[k];
-                W.len[k] = wp[3 + k];
-            }
-            pop_fill_slot<true, true>(A, T, s, i, base, pos, p0, lrow + t * (ROW / 2), ROW - 2, &W);
-        } else {
-            pop_fill_slot<true>(A, T, s, i, base, pos, p0, lrow + t * (ROW / 2), ROW - 2);
-        }
-    } else {
+    if (p0.w >= 0.0f)
+        pop_fill_slot<true>(A, T, s, i, base, pos, p0, lrow + t * (ROW / 2), ROW - 2);
+    else
         T.nnb[base + i] = 0;
-    }
 }
-
 
 // Two-level lists: the inner Verlet list (cut_in) of every slot of a structure whose
 // inner list is rebuilt this step, filtered from its outer list (no cell walk, no new
@@ -2599,17 +2352,12 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
                     for (int u = 0; u < 2 * U; ++u) pair2(pt[2 * u], pt[2 * u + 1]);
                 }
             };
-#ifndef IGM_TIMING_NOPAIRS
             pairs([&](uint32_t j) { return pop_ld(rp, j); });
-#endif
             fx = ax.x + ax.y;
             fy = ay.x + ay.y;
             fz = az.x + az.y;
         }
     }
-#ifdef IGM_TIMING_NOBONDS
-    deg = 0;
-#endif
     for (int k0 = 0; k0 < deg; k0 += 4) {
         uint32_t et[4];
         if (rebuilt) {  // atom-space entries -> slot-space (the permute of the unfused engine)
@@ -2743,227 +2491,6 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
     }
 }
 
-#ifndef IGM_POP_WFORCE_OCC
-#define IGM_POP_WFORCE_OCC 7  // waves per SIMD: 7 workgroups of 22.4 KB window per CU
-#endif
-
-// The global inputs of one slot of the window force kernel, loaded before the window's
-// staging so that both are one memory round trip: the slot's position, list length, bond
-// count, first list quads and first two bond chunks.
-constexpr int kWQD = IGM_POP_QDEPTH + 1;  // list quads in flight
-struct WSlot {
-    float4 p0;
-    int nn, deg;
-    uint2 qb[kWQD];
-    uint4 eb[2];
-};
-
-__device__ __forceinline__ void pop_wslot_load(const PopArgs& A, int s, int i, size_t base, const float4* pos,
-                                               WSlot& L) {
-    const int nsl = A.cm.nslice;
-    const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
-    const uint4* gb = reinterpret_cast<const uint4*>(A.bnt) + ((size_t)s * nsl + (i >> 6)) * A.kb4 * 64 + (i & 63);
-    L.p0 = pos[i];
-    L.nn = A.nnb[base + i];
-    L.deg = A.bdegb[A.par[s]][base + i];
-    const int nq = L.nn == kNnbWalk ? 0 : (L.nn + 3) >> 2;
-#pragma unroll
-    for (int d = 0; d < kWQD; ++d) L.qb[d] = d < nq ? gl[(size_t)d * 64] : make_uint2(0u, 0u);
-    L.eb[0] = L.deg > 0 ? gb[0] : make_uint4(0u, 0u, 0u, 0u);
-    L.eb[1] = L.deg > 4 ? gb[64] : make_uint4(0u, 0u, 0u, 0u);
-}
-
-// f32 force on slot i with the block's window in LDS (window-form entries): the
-// pop_slot_force arithmetic on the same neighbours in the same order, with every neighbour
-// and bond partner in the window one LDS read (`win`: the window's positions of this
-// step); an entry outside the window (a clipped window, a distant bond partner) is read
-// from HBM.
-__device__ __forceinline__ void pop_slot_wforce(const PopArgs& A, int s, int i, size_t base, const float4* pos,
-                                                const float4* win, WSlot& L, uint32_t fl, float evf, float envf,
-                                                float& fx, float& fy, float& fz) {
-    const int nsl = A.cm.nslice;
-    const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
-    const uint4* gb = reinterpret_cast<const uint4*>(A.bnt) + ((size_t)s * nsl + (i >> 6)) * A.kb4 * 64 + (i & 63);
-    const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
-    const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
-    const float4 p0 = L.p0;
-    const float xi = p0.x, yi = p0.y, zi = p0.z, ri = p0.w;
-    fx = fy = fz = 0.0f;
-    const float evfpi = evf * 0.318309886183790671537767526745f;
-    const int nn = L.nn, deg = L.deg;
-    // a window entry: one LDS read; past the window (rare) the HBM read replaces it
-    auto fetch = [&](uint32_t e) -> float4 {
-        float4 v = win[e < (uint32_t)kWinCap ? e : 0u];
-        if (e >= (uint32_t)kWinCap) v = pop_ld(rp, e - (uint32_t)kWinCap);
-        return v;
-    };
-    pop_f2 ax = {0.0f, 0.0f}, ay = {0.0f, 0.0f}, az = {0.0f, 0.0f};
-    auto pair2 = [&](const float4& a, const float4& b) {
-        const pop_f2 dx = pop_f2{xi, xi} - pop_f2{a.x, b.x}, dy = pop_f2{yi, yi} - pop_f2{a.y, b.y},
-                     dz = pop_f2{zi, zi} - pop_f2{a.z, b.z};
-        const pop_f2 r2 = dx * dx + dy * dy + dz * dz;
-        const pop_f2 rc = pop_f2{ri, ri} + pop_f2{a.w, b.w};
-        const pop_f2 rc2 = rc * rc;
-        const pop_f2 q = (r2 + 1.0e-20f) * rc2;
-        const pop_f2 t = {__builtin_amdgcn_rsqf(q.x), __builtin_amdgcn_rsqf(q.y)};
-        const pop_f2 h = (0.5f * r2) * t;
-        const pop_f2 sn = {__builtin_amdgcn_sinf(h.x), __builtin_amdgcn_sinf(h.y)};
-        const pop_f2 f = (evfpi * rc2) * (sn * t);
-        const pop_f2 m = {r2.x < rc2.x ? f.x : 0.0f, r2.y < rc2.y ? f.y : 0.0f};
-        ax += m * dx;
-        ay += m * dy;
-        az += m * dz;
-    };
-    if (ri >= 0.0f) {
-        if (nn == kNnbWalk) {
-            const pop_f3 b = A.xb[base + i];
-            const float4 f = pop_walk_pairs(pos, A.cell + (size_t)s * kPopCells, A.gp + (size_t)s * 8,
-                                            A.gn + (size_t)s * 8, b.x, b.y, b.z, i, p0, evfpi);
-            fx = f.x;
-            fy = f.y;
-            fz = f.z;
-        } else {
-            const int nq = (nn + 3) >> 2;
-            for (int q = 0; q < nq; ++q) {
-                const uint2 e = L.qb[0];
-#pragma unroll
-                for (int d = 0; d + 1 < kWQD; ++d) L.qb[d] = L.qb[d + 1];
-                if (q + kWQD < nq) L.qb[kWQD - 1] = gl[(size_t)(q + kWQD) * 64];
-                const float4 a0 = fetch(e.x & 0xffffu), a1 = fetch(e.x >> 16), a2 = fetch(e.y & 0xffffu),
-                             a3 = fetch(e.y >> 16);
-                pair2(a0, a1);
-                pair2(a2, a3);
-            }
-            fx = ax.x + ax.y;
-            fy = ay.x + ay.y;
-            fz = az.x + az.y;
-        }
-    }
-    float bfx = 0.0f, bfy = 0.0f, bfz = 0.0f;  // the bonds' sum
-    const int nb4 = (deg + 3) >> 2;
-    for (int c = 0; c < nb4; ++c) {
-        const uint4 et = L.eb[0];
-        L.eb[0] = L.eb[1];
-        if (c + 2 < nb4) L.eb[1] = gb[(size_t)(c + 2) * 64];
-        const uint32_t e4[4] = {et.x, et.y, et.z, et.w};
-        float4 pt[4];
-        float2 ct[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            pt[u] = fetch(e4[u] & 0xffffu);
-            ct[u] = bt[(e4[u] >> 16) & 0x7fffu];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {  // (a padding entry is the slot itself: r2 = 0 adds nothing)
-            const float dx = xi - pt[u].x, dy = yi - pt[u].y, dz = zi - pt[u].z;
-            const float r2 = dx * dx + dy * dy + dz * dz;
-            const float rinv = __builtin_amdgcn_rsqf(fmaxf(r2, 1.0e-30f));
-            const float dr = r2 * rinv - ct[u].x;
-            const bool active = (e4[u] & kLowerBit) ? (dr < 0.0f) : (dr > 0.0f);
-            const float m = (active && r2 > 0.0f) ? -2.0f * ct[u].y * dr * rinv : 0.0f;
-            bfx += m * dx;
-            bfy += m * dy;
-            bfz += m * dz;
-        }
-    }
-    fx += bfx;
-    fy += bfy;
-    fz += bfz;
-    // envelopes (non-bead atoms carry -(radius + 1))
-    const float rad = ri >= 0.0f ? ri : -ri - 1.0f;
-    for (int e = 0; e < A.P.nenv; ++e) {
-        if (!(fl & (IGM_ATOM_ENV0 << e))) continue;
-        if (A.P.env_kind[e] == IGM_ENV_VOLUME) {
-            double en = 0.0;
-            volume_term<float, false>(xi, yi, zi, A.P.vmaps[A.P.vsmap ? A.P.vsmap[s] : 0], A.P.vvox, envf,
-                                      A.P.env_k[e], fx, fy, fz, en);
-            continue;
-        }
-        const float k = A.P.env_k[e];
-        const float sx = A.P.env_abc[e][0] * envf - rad, sy = A.P.env_abc[e][1] * envf - rad,
-                    sz = A.P.env_abc[e][2] * envf - rad;
-        const float ix = __builtin_amdgcn_rcpf(sx * sx), iy = __builtin_amdgcn_rcpf(sy * sy),
-                    iz = __builtin_amdgcn_rcpf(sz * sz);
-        const float k2 = xi * xi * ix + yi * yi * iy + zi * zi * iz;
-        const bool active = (k > 0.0f) ? (k2 > 1.0f) : (k2 < 1.0f && k2 > 0.0f);
-        if (!active) continue;
-        const float r2 = xi * xi + yi * yi + zi * zi;
-        const float rinv = __builtin_amdgcn_rsqf(r2), rsk = __builtin_amdgcn_rsqf(k2);
-        const float rn = r2 * rinv;
-        const float t = (1.0f - rsk) * rn;
-        const float ca = (1.0f - rsk) * rinv, cb = rn * rsk * __builtin_amdgcn_rcpf(k2);
-        const float ka = fabsf(k);
-        fx -= ka * t * (ca * xi + cb * xi * ix);
-        fy -= ka * t * (ca * yi + cb * yi * iy);
-        fz -= ka * t * (ca * zi + cb * zi * iz);
-    }
-    if (fl & IGM_ATOM_FIXED) fx = fy = fz = 0.0f;  // fix setforce 0 (lammps.py:222-223)
-}
-
-// pop_force_kernel with the block's window (A.win, written at the last list build) staged
-// in LDS: one coalesced read of ~1 100 slots per 256-slot block (config C) replaces the ~20
-// L1 tag lookups per slot of the neighbour and bond-partner gathers, which kept the
-// texture path 90 % busy (profiles/r05_mem).  The slot's own loads, list quads and bond
-// chunks are issued with the staging loads (one round trip before the barrier).
-__global__ void __launch_bounds__(kPopBS, IGM_POP_WFORCE_OCC) pop_wforce_kernel(PopArgs A, float evf, float envf,
-                                                                              PopStep S) {
-    __shared__ float4 win[kWinCap];
-    __shared__ double red[kPopBS / 64];
-    const int lb = pop_block(), s = lb / A.nbs, blk = lb % A.nbs, i = blk * kPopBS + threadIdx.x;
-    if (s >= A.cm.nstruct) return;
-    if (lb == 0 && threadIdx.x == 0) *A.nflag = 0;  // the build kernels of this step are done
-    const int rebuilt = A.flag[S.fp][s];
-    if (i == 0) {
-        A.nrebuild[s] += rebuilt ? 1 : 0;
-        A.flag[S.fp ^ 1][s] = 0;  // the next step's flags start clear
-        A.oflag[S.fp ^ 1][s] = 0;
-    }
-    const size_t base = (size_t)s * A.cm.ldn, k = base + i;
-    const PopBuf& B = A.buf[A.par[s]];
-    const float4* pos = B.pos + base;
-    const bool live = i < A.cm.natom;
-    WSlot L;
-    pop_f3 v = {0.f, 0.f, 0.f};
-    uint32_t fl = 0;
-    if (live) {
-        pop_wslot_load(A, s, i, base, pos, L);
-        v = B.vel[k];
-        fl = B.flg[k];
-    }
-    {
-        const int* wp = A.win + ((size_t)s * A.nbs + blk) * 8;
-        PopWin W;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            W.lo[q] = __builtin_amdgcn_readfirstlane(wp[q]);
-            W.len[q] = __builtin_amdgcn_readfirstlane(wp[3 + q]);
-        }
-        const int tot = W.len[0] + W.len[1] + W.len[2];
-        for (int q = threadIdx.x; q < tot; q += kPopBS) win[q] = pos[pop_win_slot(W, q)];
-    }
-    __syncthreads();
-    double ke = 0.0;
-    if (live) {
-        float fx, fy, fz;
-        pop_slot_wforce(A, s, i, base, pos, win, L, fl, evf, envf, fx, fy, fz);
-        B.frc[k] = pop_f3{fx, fy, fz};
-        if (S.integrate && !(fl & IGM_ATOM_FIXED)) {
-            kick_limit(v.x, v.y, v.z, fx, fy, fz, S.dtf, S.vlim, S.vlimsq);
-            ke = (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z);
-        }
-    }
-    if (!S.integrate) return;
-    ke = wave_sum_f64(ke);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ke;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-#pragma unroll
-        for (int w = 0; w < kPopBS / 64; ++w) t += red[w];
-        A.kep[(size_t)s * A.nbs + blk] = t;
-    }
-}
-
 // end of a run: the last step's rescale, then (optionally) the outputs in atom order
 __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S, float* xyz, float* vel,
                                                             float* forces_out) {
@@ -3070,45 +2597,6 @@ __global__ void __launch_bounds__(kPopBS) pop_stats_kernel(PopArgs A, unsigned l
         atomicAdd(&st[13], span > 3072 ? 1ull : 0ull);
         atomicAdd(&st[14], span > 4096 ? 1ull : 0ull);
         atomicAdd(&st[15], (unsigned long long)nin);
-    }
-}
-
-// Tuning diagnostic (IGM_POP_STATS, second pass): the three per-layer slot intervals
-// of every 256-slot block (pop_block_window) -- total slots, how many of the block's
-// list entries fall inside -- as a histogram of totals.
-__global__ void __launch_bounds__(kPopBS) pop_wstats_kernel(PopArgs A, unsigned long long* st) {
-    const int lb = pop_block(), s = lb / A.nbs, b = lb % A.nbs, i = b * kPopBS + threadIdx.x;
-    if (s >= A.cm.nstruct) return;
-    __shared__ PopWin W;
-    __shared__ int nin, ntot;
-    if (threadIdx.x == 0) {
-        W = pop_block_window(A, s, b, 1 << 20);
-        nin = ntot = 0;
-    }
-    __syncthreads();
-    const size_t base = (size_t)s * A.cm.ldn;
-    int nn = i < A.cm.natom ? A.nnb[base + i] : 0;
-    if (nn == kNnbWalk) nn = 0;
-    const uint2* gl = A.nl + ((size_t)s * A.cm.nslice + (i >> 6)) * A.kq * 64 + (i & 63);
-    int in = 0;
-    for (int q = 0; q < (nn + 3) >> 2; ++q) {
-        const uint2 e = gl[(size_t)q * 64];
-        const int j4[4] = {(int)(e.x & 0xffffu), (int)(e.x >> 16), (int)(e.y & 0xffffu), (int)(e.y >> 16)};
-        for (int u = 0; u < 4 && 4 * q + u < nn; ++u) in += pop_win_index(W, j4[u]) >= 0 ? 1 : 0;
-    }
-    atomicAdd(&nin, in);
-    atomicAdd(&ntot, nn);
-    __syncthreads();
-    if (threadIdx.x == 0 && W.len[0] + W.len[1] + W.len[2] > 0) {
-        const int T = W.len[0] + W.len[1] + W.len[2];
-        atomicAdd(&st[0], (unsigned long long)T);
-        atomicAdd(&st[1], 1ull);
-        atomicMax(&st[2], (unsigned long long)T);
-        atomicAdd(&st[3], T > 1536 ? 1ull : 0ull);
-        atomicAdd(&st[4], T > 2048 ? 1ull : 0ull);
-        atomicAdd(&st[5], T > 3072 ? 1ull : 0ull);
-        atomicAdd(&st[6], (unsigned long long)nin);
-        atomicAdd(&st[7], (unsigned long long)ntot);
     }
 }
 
@@ -4129,10 +3617,6 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     V.dofs = Q.dofs + s0;
     V.coff = Q.coff + (size_t)s0 * (Q.cm.natom + 1);
     V.cbase = Q.cbase + s0;
-    if (Q.win) {
-        V.win = Q.win + (size_t)s0 * Q.nbs * 8;
-        V.bnt = Q.bnt + (size_t)s0 * nsl * Q.kb4 * 64 * 4;
-    }
     return V;
 }
 
@@ -4199,9 +3683,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     float margin = 0.0f;
     if (const char* e = getenv("IGM_POP_OUTER")) margin = (float)atof(e) * rmax0;
     if (kPopFused) margin = 0.0f;
-    const char* ew = getenv("IGM_POP_WIN");
-    const bool wmode = (ew ? atoi(ew) != 0 : IGM_POP_WIN_DEFAULT != 0) && N + kWinCap <= 0xFFFF && !kPopFused;
-    Q.two = margin > 0.0f && !wmode ? 1 : 0;
+    Q.two = margin > 0.0f ? 1 : 0;
     constexpr int kOuterRow = kPopOuterCap + 2;
     {
         void *pfl2, *pfli2;
@@ -4232,16 +3714,6 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.bentb[1] = (uint32_t*)pbent + SL * Q.bdmax;
     Q.bdegb[0] = (uint16_t*)pbdeg;
     Q.bdegb[1] = (uint16_t*)pbdeg + SL;
-    // block windows (default; IGM_POP_WIN=0: the plain-gather kernels, for A/B): list
-    // entries and bond partners are window entries, kWinCap + slot at most 65 535
-    if (wmode) {
-        void *pw, *pbn;
-        Q.kb4 = (Q.bdmax + 3) / 4;
-        IGM_TRY(workspace(c, "pop_win", sizeof(int) * 8 * (size_t)S * Q.nbs, &pw));
-        IGM_TRY(workspace(c, "pop_bnt", sizeof(uint32_t) * 4 * SL * Q.kb4, &pbn));
-        Q.win = (int*)pw;
-        Q.bnt = (uint32_t*)pbn;
-    }
     Q.flag[0] = (int*)pfl;
     Q.flag[1] = (int*)pfl + S;
     Q.flist = (int*)pfli;
@@ -4342,8 +3814,8 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     unsigned long long* pst = nullptr;
     if (stats_every > 0) {
         void* p;
-        IGM_TRY(workspace(c, "pop_stats", sizeof(unsigned long long) * 32 * 2 * IGM_MAX_STAGES, &p));
-        IGM_HIP_CHECK(c, hipMemsetAsync(p, 0, sizeof(unsigned long long) * 32 * 2 * IGM_MAX_STAGES, c->stream));
+        IGM_TRY(workspace(c, "pop_stats", sizeof(unsigned long long) * 16 * 2 * IGM_MAX_STAGES, &p));
+        IGM_HIP_CHECK(c, hipMemsetAsync(p, 0, sizeof(unsigned long long) * 16 * 2 * IGM_MAX_STAGES, c->stream));
         pst = (unsigned long long*)p;
     }
     Timed tm(c, "anneal");
@@ -4425,16 +3897,9 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                         } else if (!kPopFused) {
                             hipLaunchKernelGGL(pop_fill_kernel<kPopListRow>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
                         }
-                        if (wmode)
-                            hipLaunchKernelGGL(pop_wforce_kernel, grid_of(g), blk, 0, sg, V[g], evf, envf, st);
-                        else
-                            hipLaunchKernelGGL(pop_force_kernel<kPopFused>, grid_of(g), blk, 0, sg, V[g], evf, envf, st);
+                        hipLaunchKernelGGL(pop_force_kernel<kPopFused>, grid_of(g), blk, 0, sg, V[g], evf, envf, st);
                         if (pst && step % stats_every == 0)
-                        {
-                            hipLaunchKernelGGL(pop_stats_kernel, grid_of(g), blk, 0, sg, V[g], pst + 32 * seg);
-                            if (!wmode)  // (its window test reads slot-id entries)
-                                hipLaunchKernelGGL(pop_wstats_kernel, grid_of(g), blk, 0, sg, V[g], pst + 32 * seg + 16);
-                        }
+                            hipLaunchKernelGGL(pop_stats_kernel, grid_of(g), blk, 0, sg, V[g], pst + 16 * seg);
                     }
                 }
             }
@@ -4452,27 +3917,21 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     IGM_HIP_CHECK(c, hipGetLastError());
     IGM_TRY(aux_join(c, nc));
     if (pst) {
-        std::vector<unsigned long long> v(32 * 2 * IGM_MAX_STAGES);
+        std::vector<unsigned long long> v(16 * 2 * IGM_MAX_STAGES);
         IGM_HIP_CHECK(c, hipMemcpyAsync(v.data(), pst, sizeof(unsigned long long) * v.size(), hipMemcpyDeviceToHost,
                                         c->stream));
         IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
         for (int seg = 0; seg < A.nseg; ++seg) {
-            const unsigned long long* u = v.data() + 32 * seg;
+            const unsigned long long* u = v.data() + 16 * seg;
             const double n = (double)(u[0] ? u[0] : 1), w = (double)(u[7] ? u[7] : 1), m = u[1] / n;
+            const double nb = (double)(u[10] ? u[10] : 1);
             fprintf(stderr, "[igm pop stats] run %d T0 %.0f skin %.3f rmax: list mean %.2f sd %.2f max %llu, wave-max "
-                            "quads %.2f (mean quads %.2f), walks %.2e, bonds mean %.2f wave-max %.2f\n",
+                            "quads %.2f (mean quads %.2f), walks %.2e, bonds mean %.2f wave-max %.2f; block slot span "
+                            "mean %.0f max %llu (>2048 %.4f, >3072 %.4f, >4096 %.4f), bonds inside it %.4f\n",
                     seg, A.seg_t0[seg], seg_skin[seg] / (0.5f * (pr.P.cut_list - pr.P.skin)), m,
                     sqrt(fmax(u[2] / n - m * m, 0.0)), u[8], u[5] / w, (u[1] + 3.0 * u[0]) / 4.0 / n, u[3] / n,
-                    u[4] / n, u[6] / w);
-            const double nb = (double)(u[10] ? u[10] : 1);
-            fprintf(stderr, "[igm pop stats] run %d block windows: span mean %.0f max %llu, >2048 %.4f >3072 %.4f "
-                            ">4096 %.4f; bonds inside %.4f\n",
-                    seg, u[9] / nb, u[11], u[12] / nb, u[13] / nb, u[14] / nb, u[15] / (double)(u[4] ? u[4] : 1));
-            const unsigned long long* x = u + 16;
-            const double nw = (double)(x[1] ? x[1] : 1);
-            fprintf(stderr, "[igm pop stats] run %d 3-interval windows: slots mean %.0f max %llu, >1536 %.4f >2048 %.4f "
-                            ">3072 %.4f; list entries inside %.4f\n",
-                    seg, x[0] / nw, x[2], x[3] / nw, x[4] / nw, x[5] / nw, x[6] / (double)(x[7] ? x[7] : 1));
+                    u[4] / n, u[6] / w, u[9] / nb, u[11], u[12] / nb, u[13] / nb, u[14] / nb,
+                    u[15] / (double)(u[4] ? u[4] : 1));
         }
     }
     if (sprof) {

@@ -71,7 +71,7 @@ def _mlib():
         L.oracle_mstep_forces.restype = ctypes.c_int
         L.oracle_mstep_forces.argtypes = [vp, i32, i32, vp, vp, vp, vp, i64, vp, vp, f64, f64, vp, vp]
         L.oracle_mstep_md.restype = ctypes.c_int
-        L.oracle_mstep_md.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, i64, vp, vp, f64, f64, f64, f64, f64, i32]
+        L.oracle_mstep_md.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, i64, vp, vp, f64, f64, f64, f64, f64, i32, i32]
         L.oracle_velocity_create.restype = ctypes.c_int
         L.oracle_velocity_create.argtypes = [i32, vp, f64, i32, vp]
         L.oracle_hic_select.restype = ctypes.c_int
@@ -148,7 +148,7 @@ def mstep_forces(params, xyz, radii, flags, shared, sptr, sbonds, evf, envf):
     return f, e
 
 
-def mstep_md(params, x, v, radii, flags, shared, sptr, sbonds, evf, envf, t0, t1, xmax, nsteps):
+def mstep_md(params, x, v, radii, flags, shared, sptr, sbonds, evf, envf, t0, t1, xmax, nsteps, nthreads=1):
     import ctypes as C
     x = np.array(x, np.float64, order='C')
     v = np.array(v, np.float64, order='C')
@@ -159,7 +159,7 @@ def mstep_md(params, x, v, radii, flags, shared, sptr, sbonds, evf, envf, t0, t1
     _mlib().oracle_mstep_md(C.byref(params), S, N, x.ctypes.data, v.ctypes.data, radii.ctypes.data,
                             flags.ctypes.data, shared.ctypes.data, len(shared), sptr.ctypes.data,
                             sbonds.ctypes.data, float(evf), float(envf), float(t0), float(t1), float(xmax),
-                            int(nsteps))
+                            int(nsteps), int(nthreads))
     return x, v
 
 

@@ -757,9 +757,10 @@ int oracle_mstep_forces(const igm_mstep_params* p, int32_t nstruct, int32_t nato
 int oracle_mstep_md(const igm_mstep_params* p, int32_t nstruct, int32_t natom, double* x, double* v,
                     const float* radii, const uint32_t* fl, const igm_bond* shared, int64_t nshared,
                     const int64_t* sptr, const igm_bond* sbonds, double evf, double envf, double t0, double t1,
-                    double xmax, int32_t nsteps) {
-    float* xf = (float*)malloc(sizeof(float) * 3 * natom);
+                    double xmax, int32_t nsteps, int32_t nthreads) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
     for (int s = 0; s < nstruct; ++s) {
+        float* xf = (float*)malloc(sizeof(float) * 3 * natom);
         model_t m;
         const int64_t b0 = sptr ? sptr[s] : 0, b1 = sptr ? sptr[s + 1] : 0;
         for (int i = 0; i < 3 * natom; ++i) xf[i] = (float)x[(size_t)s * natom * 3 + i];
@@ -773,8 +774,8 @@ int oracle_mstep_md(const igm_mstep_params* p, int32_t nstruct, int32_t natom, d
         memcpy(x + (size_t)s * natom * 3, m.x, sizeof(double) * 3 * natom);
         memcpy(v + (size_t)s * natom * 3, m.v, sizeof(double) * 3 * natom);
         model_free(&m);
+        free(xf);
     }
-    free(xf);
     return 0;
 }
 

@@ -195,33 +195,6 @@ def test_gpu_200kb_small_list_capacity_forces_match_oracle(ms, model200):
     assert np.linalg.norm(err) <= 1e-5 * np.linalg.norm(np.linalg.norm(fo, axis=2))
 
 
-@pytest.mark.parametrize('scale', [1.0, 0.4])
-def test_gpu_200kb_window_engine_equals_gather_engine(ms, model200, scale, monkeypatch):
-    """The block-window kernels (pop_wfill / pop_wforce: neighbour and bond-partner
-    positions read from the block's slot window staged in LDS) sum the same neighbours in
-    the same order as the plain-gather kernels (IGM_POP_WIN=0): f32 forces equal to
-    rounding (the compiler contracts the two kernels' sums differently), and an MD segment
-    with list rebuilds stays within 1e-5 of the coordinate scale (velocities 1e-4).  Scale 0.4: a compressed
-    structure whose dense blocks clip their windows at kWinCap (entries outside read from
-    HBM) and whose longest lists take the cell walk; its overlapping beads make the MD
-    chaotic within a few steps, so it runs 5."""
-    atoms, poly, prm, ptr, sb, x = model200
-    xc = x.copy()
-    xc[:, :atoms.nbead] *= scale
-    v = np.stack([oracle.velocity_create(atoms.flags, 400.0, 31 + s) for s in range(2)]).astype(np.float32)
-    out, frc = [], []
-    for mode in ('0', '1'):
-        monkeypatch.setenv('IGM_POP_WIN', mode)
-        frc.append(ms.forces(prm, xc, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2, f32=True)[0])
-        out.append(ms.md(prm, xc, v, atoms.radii, atoms.flags, poly, ptr, sb, 0.5, 1.2, 400.0, 300.0, 1000.0,
-                         40 if scale == 1.0 else 5))
-    assert np.abs(frc[0] - frc[1]).max() <= 1e-6 * np.abs(frc[0]).max()
-    (xa, va), (xb, vb) = out
-    assert np.abs(xa - xc).max() > 1.0
-    assert np.abs(xa - xb).max() <= 1e-5 * np.abs(xa).max()
-    assert np.abs(va - vb).max() <= 1e-4 * np.abs(va).max()
-
-
 @pytest.mark.parametrize('engine', ['lds', 'hbm'])
 def test_gpu_retired_engine_flag_is_rejected(demo, ms, engine):
     """params flag 0x4 (round 3's domain-decomposed engine) is retired: igm_mstep_run returns
