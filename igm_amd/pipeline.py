@@ -128,17 +128,21 @@ class AMIteration(object):
 
     def __init__(self, device, xyz_local, atoms, chrom, copy_ptr, copy_idx, pairs, params, polymer,
                  seed=6535, contact_range=2.0, kspring=1.0, it_corr=1, tol=0.05, env_scale=(550.0,),
-                 first_sid=0, rank=0, world=1, group=None):
+                 first_sid=0, rank=0, world=1, group=None, collective=None):
+        """collective: run the N > 1 exchange (population all-gather, row gather, score
+        all-reduce) through torch.distributed; default world > 1.  True at world 1 puts a
+        single rank through the same collectives (the one-GPU RCCL test)."""
         import torch
         self.torch = torch
         self.dev = torch.device(device)
         self.rank, self.world, self.group = rank, world, group
+        self.coll = world > 1 if collective is None else bool(collective)
         self.ctx = _lib.context(self.dev.index or 0)
         T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a if dt is None else a.astype(dt))).to(self.dev)
         xyz_local = np.ascontiguousarray(xyz_local, np.float32)
         self.S_local, self.natom = xyz_local.shape[0], xyz_local.shape[1]
         self.nbead = int(atoms.nbead)
-        if world > 1:  # gather_population all-gathers equal blocks: every rank must hold as many structures
+        if self.coll:  # gather_population all-gathers equal blocks: every rank must hold as many structures
             counts = self._all_counts(self.S_local)
             if len(set(counts)) != 1:
                 raise ValueError('structure shards must be equal (got %s per rank): pad the population to a '
@@ -201,7 +205,7 @@ class AMIteration(object):
     def astep(self):
         torch = self.torch
         P = _lib.ptr
-        if self.world > 1:
+        if self.coll:
             src = gather_population(self.xyz, self.group)
         else:
             src = self.xyz
@@ -217,7 +221,7 @@ class AMIteration(object):
                        P(self.hap_chrom), P(self.pairs), self.npairs, float(self.cr), int(self.it_corr),
                        P(self.per_pair), P(rows), cap, ctypes.byref(n))
         nrows = n.value
-        if self.world > 1:
+        if self.coll:
             rows, nrows = gather_rows(rows, nrows, row_dtype.itemsize, self.row_cap, self.group)
         self.rows, self.nrows = rows, nrows
         if self.it_corr == 1 and self.npairs > 0:  # plast of the next iteration (same sigma)
@@ -265,7 +269,7 @@ class AMIteration(object):
     def violation_score(self):
         """ModelingStep.log_stats: sum n_violations / sum n_imposed (all ranks)."""
         nv, ni = float(self.stats[:, :, 102].sum()), float(self.stats[:, :, 103].sum())
-        if self.world > 1:
+        if self.coll:
             nv, ni = reduce_sum_f64([nv, ni], self.dev, self.group)
         return nv / ni if ni > 0 else 0.0
 
@@ -289,11 +293,11 @@ class AMIteration(object):
         it_corr state of ActivationDistanceStep), the non-bead atoms' coordinates."""
         from . import hss
         P = _lib.ptr
-        src = gather_population(self.xyz, self.group) if self.world > 1 else self.xyz
+        src = gather_population(self.xyz, self.group) if self.coll else self.xyz
         self._call('igm_population_transpose', IGM_DEVICE_PTRS, self.nbead, self.S_total, self.natom, P(src),
                    P(self.pop_bm), 1)
         pairs_u8 = self.pairs[:self.npairs * pair_dtype.itemsize]
-        if self.world > 1:
+        if self.coll:
             cap = max(hi - lo for lo, hi in (shard_weighted(self._combos, r, self.world) for r in range(self.world)))
             pairs_u8, np_tot = gather_rows(pairs_u8, self.npairs, pair_dtype.itemsize, cap, self.group)
             pairs_u8 = pairs_u8[:np_tot * pair_dtype.itemsize]

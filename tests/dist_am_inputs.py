@@ -31,8 +31,9 @@ def inputs(nstruct=8):
     return dict(pop=pop, pairs=pairs, atoms=atoms, xyz=xyz, prm=prm, poly=poly, chrom=chrom)
 
 
-def iteration(inp, device, s0, s1, rank=0, world=1):
+def iteration(inp, device, s0, s1, rank=0, world=1, collective=None):
     from igm_amd.pipeline import AMIteration
     pop = inp['pop']
     return AMIteration(device, inp['xyz'][s0:s1], inp['atoms'], inp['chrom'], pop['copy_ptr'], pop['copy_idx'],
-                       inp['pairs'], inp['prm'], inp['poly'], first_sid=s0, rank=rank, world=world)
+                       inp['pairs'], inp['prm'], inp['poly'], first_sid=s0, rank=rank, world=world,
+                       collective=collective)

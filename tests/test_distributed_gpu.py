@@ -61,11 +61,12 @@ def test_gpu_ranks_equal_one_rank(tmp_path, world):
 
 
 def test_gpu_rccl_collectives_one_rank():
-    """The RCCL ('nccl') path of the collective helpers runs on device tensors (one rank:
+    """The RCCL ('nccl') path of the collective helpers and a whole AMIteration.step() with its
+    N > 1 exchanges run on device tensors, the step byte-equal to one without them (one rank:
     RCCL refuses two ranks on one GPU; the two-rank equality above runs over gloo)."""
     env = dict(os.environ, OMP_NUM_THREADS='2')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1',
            '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'rccl_worker.py')]
-    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=180)
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0 and 'RCCL-OK' in r.stdout, r.stdout[-4000:]
 
