@@ -50,6 +50,47 @@ __device__ __forceinline__ void load3(const float* __restrict__ xyz, int S, int 
     z = p[2];
 }
 
+// rank[t] = the position of element t in the stable ascending order of v[0..n): the
+// argsort(argsort(v)) NumPy computes (ties in index order), i.e. #{u : v[u] < v[t]} +
+// #{u < t : v[u] == v[t]}.  A bitonic sort of the (value, index) pairs in LDS -- npad (a power
+// of two >= n) keys sk and indices si, every thread of the block taking part -- in place of
+// counting every rank against the whole column (O(n^2): 1 M comparisons per FISH item at
+// n = 1000, against ~28 k compare-exchanges here).  The pad sorts after every value (+inf,
+// index >= n).
+__device__ void block_stable_rank(const float* v, int n, int npad, float* sk, int* si, int* rank) {
+    for (int p = threadIdx.x; p < npad; p += kBT) {
+        sk[p] = p < n ? v[p] : INFINITY;
+        si[p] = p;
+    }
+    __syncthreads();
+    for (int k = 2; k <= npad; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int p = threadIdx.x; p < npad; p += kBT) {
+                const int q = p ^ j;
+                if (q > p) {
+                    const float a = sk[p], b = sk[q];
+                    const int ia = si[p], ib = si[q];
+                    const bool gt = a > b || (a == b && ia > ib);
+                    if (gt == ((p & k) == 0)) {
+                        sk[p] = b;
+                        sk[q] = a;
+                        si[p] = ib;
+                        si[q] = ia;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int p = threadIdx.x; p < n; p += kBT) rank[si[p]] = p;
+    __syncthreads();
+}
+
+__host__ __device__ inline int pow2_at_least(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
 // ============================================================================ DamID
 struct DamidArgs {
     const float* xyz;
@@ -415,30 +456,25 @@ __global__ void __launch_bounds__(kBT) fish_kernel(FishArgs A) {
         vmax[s] = mx;
     }
     __syncthreads();
+    // the ranks of the column (block_stable_rank), min then max
+    const int npad = pow2_at_least(S);
+    float* sk = fsm + 2 * S;
+    int* si = reinterpret_cast<int*>(sk + npad);
+    int* rmin = si + npad;
+    int* rmax = rmin + S;
+    block_stable_rank(vmin, S, npad, sk, si, rmin);
+    block_stable_rank(vmax, S, npad, sk, si, rmax);
     const size_t row = (size_t)q * S;
     for (int s = threadIdx.x; s < S; s += kBT) {
-        const float mn = vmin[s], mx = vmax[s];
-        int rmin = 0, rmax = 0;
-        int t = 0;
-        for (; t + 4 <= S; t += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float a = vmin[t + u], b = vmax[t + u];
-                rmin += (a < mn) | ((a == mn) & (t + u < s));
-                rmax += (b < mx) | ((b == mx) & (t + u < s));
-            }
-        }
-        for (; t < S; ++t) {
-            const float a = vmin[t], b = vmax[t];
-            rmin += (a < mn) | ((a == mn) & (t < s));
-            rmax += (b < mx) | ((b == mx) & (t < s));
-        }
-        if (A.omin) A.omin[row + s] = A.tmin[row + rmin];
-        if (A.omax) A.omax[row + s] = A.tmax[row + rmax];
-        if (A.dmin) A.dmin[row + s] = mn;
-        if (A.dmax) A.dmax[row + s] = mx;
+        if (A.omin) A.omin[row + s] = A.tmin[row + rmin[s]];
+        if (A.omax) A.omax[row + s] = A.tmax[row + rmax[s]];
+        if (A.dmin) A.dmin[row + s] = vmin[s];
+        if (A.dmax) A.dmax[row + s] = vmax[s];
     }
 }
+
+// LDS of fish_kernel: the min and max columns, the sort's keys and indices, two rank columns
+inline size_t fish_lds(int S) { return sizeof(float) * (4 * (size_t)S + 2 * (size_t)pow2_at_least(S)); }
 
 // ============================================================================ SPRITE
 struct SpriteArgs {
@@ -455,10 +491,20 @@ struct SpriteArgs {
     const int* alt_bead;
     float* rg2;  // (ncl, S)
     int* sel;    // (nseg, S): the selected bead of every cluster segment
+    // flat tables of the clusters whose regions all have 1 or 2 copies (two[c]), built on the
+    // host: each segment's / representative's copy 0 and copy 1 (copy 0 again for one copy,
+    // which is then also the last copy that -1 selects) and the bit of its representative's
+    // digit in a combination index (0 for one copy: both entries are the same bead)
+    const int* ncomb2;  // 2^(2-copy representatives) of a two[c] cluster, 0 otherwise
+    const int2* seg_b2;
+    const unsigned char* seg_bit;
+    const int2* rep_b2;
+    const unsigned char* rep_bit;
 };
 
 constexpr float kSpriteInf = 100000000.0f;  // INF of cpp_sprite_assignment.cpp:4
 constexpr int kMaxReps = 16;
+constexpr int kRegReps = 8;  // representatives whose copies a SPRITE thread keeps in registers
 
 // gyration_radius_sq (cpp_sprite_assignment.cpp:49-61): float mean accumulated in
 // order and divided by float(n), then the sum of X0*X0 + X1*X1 + X2*X2 in order / n
@@ -486,6 +532,38 @@ __device__ __forceinline__ float rg2_of(const float* __restrict__ xyz, int S, in
     return __fdiv_rn(rg, fn);
 }
 
+// rg2_of with the n <= kRegBeads positions loaded into registers first (all in flight
+// together, each read once): the same sums in the same order, bit for bit
+constexpr int kRegBeads = 20;
+template <class Bead>
+__device__ __forceinline__ float rg2_regs(const float* __restrict__ xyz, int S, int s, int n, Bead bead) {
+    if (n > kRegBeads) return rg2_of(xyz, S, s, n, bead);
+    float px[kRegBeads], py[kRegBeads], pz[kRegBeads];
+#pragma unroll
+    for (int i = 0; i < kRegBeads; ++i)
+        if (i < n) load3(xyz, S, bead(i), s, px[i], py[i], pz[i]);
+    float mx = 0.0f, my = 0.0f, mz = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kRegBeads; ++i)
+        if (i < n) {
+            mx = __fadd_rn(mx, px[i]);
+            my = __fadd_rn(my, py[i]);
+            mz = __fadd_rn(mz, pz[i]);
+        }
+    const float fn = (float)n;
+    mx = __fdiv_rn(mx, fn);
+    my = __fdiv_rn(my, fn);
+    mz = __fdiv_rn(mz, fn);
+    float rg = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kRegBeads; ++i)
+        if (i < n) {
+            const float dx = __fsub_rn(px[i], mx), dy = __fsub_rn(py[i], my), dz = __fsub_rn(pz[i], mz);
+            rg = __fadd_rn(rg, __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+        }
+    return __fdiv_rn(rg, fn);
+}
+
 // Python indexing of a copy list by the selected copy: -1 (no combination below INF)
 // wraps to the last copy, as curr_beads[sel] does in sprite.pyx:268
 __device__ __forceinline__ int alt_of(const SpriteArgs& A, int region, int k) {
@@ -510,12 +588,82 @@ __global__ void __launch_bounds__(kBT) sprite_rg2_kernel(SpriteArgs A) {
     const int r0 = A.rep_ptr[c], nr = A.rep_ptr[c + 1] - r0;
     const int S = A.S;
     float best;
-    if (nr == 0) {
+    const int nc2 = A.ncomb2[c];
+    if (nc2 > 0 && nr <= kRegReps) {
+        // the tables: every bead id one uniform load, no chain of index loads per bead
+        const int2* sb = A.seg_b2 + g0;
+        if (nr == 0) {
+            const int nalt = sb[0].x != sb[0].y ? 2 : 1;
+            best = kSpriteInf;
+            int bk = 0;
+            for (int k = 0; k < nalt; ++k) {
+                float v = rg2_regs(A.xyz, S, s, ng, [&](int i) { return k ? sb[i].y : sb[i].x; });
+                v = v < kSpriteInf ? v : kSpriteInf;
+                if (k == 0 || v < best) {
+                    best = v;
+                    bk = k;
+                }
+            }
+            for (int i = 0; i < ng; ++i) A.sel[(size_t)(g0 + i) * S + s] = bk ? sb[i].y : sb[i].x;
+        } else {
+            const int2* rb = A.rep_b2 + r0;
+            const unsigned char* rbit = A.rep_bit + r0;
+            float px[kRegReps][2], py[kRegReps][2], pz[kRegReps][2];
+            int sh[kRegReps];
+#pragma unroll
+            for (int i = 0; i < kRegReps; ++i)
+                if (i < nr) {
+                    load3(A.xyz, S, rb[i].x, s, px[i][0], py[i][0], pz[i][0]);
+                    load3(A.xyz, S, rb[i].y, s, px[i][1], py[i][1], pz[i][1]);
+                    sh[i] = rbit[i];
+                }
+            float bv = kSpriteInf;
+            int bcomb = -1;
+            const float fn = (float)nr;
+            for (int k = 0; k < nc2; ++k) {  // mixed radix, representative 0 fastest
+                float mx = 0.0f, my = 0.0f, mz = 0.0f;
+#pragma unroll
+                for (int i = 0; i < kRegReps; ++i)
+                    if (i < nr) {
+                        const int ci = (k >> sh[i]) & 1;
+                        mx = __fadd_rn(mx, ci ? px[i][1] : px[i][0]);
+                        my = __fadd_rn(my, ci ? py[i][1] : py[i][0]);
+                        mz = __fadd_rn(mz, ci ? pz[i][1] : pz[i][0]);
+                    }
+                mx = __fdiv_rn(mx, fn);
+                my = __fdiv_rn(my, fn);
+                mz = __fdiv_rn(mz, fn);
+                float rg = 0.0f;
+#pragma unroll
+                for (int i = 0; i < kRegReps; ++i)
+                    if (i < nr) {
+                        const int ci = (k >> sh[i]) & 1;
+                        const float dx = __fsub_rn(ci ? px[i][1] : px[i][0], mx),
+                                    dy = __fsub_rn(ci ? py[i][1] : py[i][0], my),
+                                    dz = __fsub_rn(ci ? pz[i][1] : pz[i][0], mz);
+                        rg = __fadd_rn(rg, __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+                    }
+                const float v = __fdiv_rn(rg, fn);
+                if (v < bv) {
+                    bv = v;
+                    bcomb = k;
+                }
+            }
+            // each segment with its chromosome's selected copy; no combination below INF
+            // (bcomb -1, all bits set) selects the last copy, .y
+            const unsigned char* sbit = A.seg_bit + g0;
+            const unsigned m = (unsigned)bcomb;
+            auto bead = [=](int i) { return (m >> sbit[i]) & 1u ? sb[i].y : sb[i].x; };
+            for (int i = 0; i < ng; ++i) A.sel[(size_t)(g0 + i) * S + s] = bead(i);
+            best = rg2_regs(A.xyz, S, s, ng, bead);
+            best = best < kSpriteInf ? best : kSpriteInf;
+        }
+    } else if (nr == 0) {
         const int nalt = A.alt_ptr[A.seg_region[g0] + 1] - A.alt_ptr[A.seg_region[g0]];
         best = kSpriteInf;
         int bk = 0;
         for (int k = 0; k < nalt; ++k) {
-            float v = rg2_of(A.xyz, S, s, ng, [&](int i) { return alt_of(A, A.seg_region[g0 + i], k); });
+            float v = rg2_regs(A.xyz, S, s, ng, [&](int i) { return alt_of(A, A.seg_region[g0 + i], k); });
             v = v < kSpriteInf ? v : kSpriteInf;
             if (k == 0 || v < best) {
                 best = v;
@@ -524,27 +672,77 @@ __global__ void __launch_bounds__(kBT) sprite_rg2_kernel(SpriteArgs A) {
         }
         for (int i = 0; i < ng; ++i) A.sel[(size_t)(g0 + i) * S + s] = alt_of(A, A.seg_region[g0 + i], bk);
     } else {
-        int ncomb = 1;
-        int nalt[kMaxReps];
+        int ncomb = 1, two = 1;
+        int nalt[kMaxReps], bit[kMaxReps];  // bit: position of representative i's copy digit (copies <= 2)
         for (int i = 0; i < nr; ++i) {
             const int rg = A.rep_region[r0 + i];
             nalt[i] = A.alt_ptr[rg + 1] - A.alt_ptr[rg];
+            bit[i] = 0;
+            two &= nalt[i] >= 1 && nalt[i] <= 2;
             ncomb *= nalt[i];
         }
         float bv = kSpriteInf;
         int bcomb = -1;
-        for (int k = 0; k < ncomb; ++k) {
-            const float v = rg2_of(A.xyz, S, s, nr, [&](int i) {
-                int kk = k, ci = 0;
-                for (int j = 0; j <= i; ++j) {
-                    ci = kk % nalt[j];
-                    kk /= nalt[j];
+        if (two && nr <= kRegReps) {
+            // Every combination reads the same 2 nr bead columns: load them once (all in
+            // flight together) and form the combinations from registers, in the reference's
+            // order and arithmetic (mixed radix with copies <= 2: digit i is bit bit[i] of k).
+            float px[kRegReps][2], py[kRegReps][2], pz[kRegReps][2];
+            int b = 0;
+#pragma unroll
+            for (int i = 0; i < kRegReps; ++i) {
+                if (i < nr) {
+                    const int rg = A.rep_region[r0 + i];
+                    load3(A.xyz, S, alt_of(A, rg, 0), s, px[i][0], py[i][0], pz[i][0]);
+                    load3(A.xyz, S, alt_of(A, rg, nalt[i] - 1), s, px[i][1], py[i][1], pz[i][1]);
+                    bit[i] = b;
+                    b += nalt[i] - 1;
                 }
-                return alt_of(A, A.rep_region[r0 + i], ci);
-            });
-            if (v < bv) {
-                bv = v;
-                bcomb = k;
+            }
+            const float fn = (float)nr;
+            for (int k = 0; k < ncomb; ++k) {
+                float mx = 0.0f, my = 0.0f, mz = 0.0f;
+#pragma unroll
+                for (int i = 0; i < kRegReps; ++i)
+                    if (i < nr) {
+                        const int ci = (k >> bit[i]) & (nalt[i] - 1);
+                        mx = __fadd_rn(mx, ci ? px[i][1] : px[i][0]);
+                        my = __fadd_rn(my, ci ? py[i][1] : py[i][0]);
+                        mz = __fadd_rn(mz, ci ? pz[i][1] : pz[i][0]);
+                    }
+                mx = __fdiv_rn(mx, fn);
+                my = __fdiv_rn(my, fn);
+                mz = __fdiv_rn(mz, fn);
+                float rg = 0.0f;
+#pragma unroll
+                for (int i = 0; i < kRegReps; ++i)
+                    if (i < nr) {
+                        const int ci = (k >> bit[i]) & (nalt[i] - 1);
+                        const float dx = __fsub_rn(ci ? px[i][1] : px[i][0], mx),
+                                    dy = __fsub_rn(ci ? py[i][1] : py[i][0], my),
+                                    dz = __fsub_rn(ci ? pz[i][1] : pz[i][0], mz);
+                        rg = __fadd_rn(rg, __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+                    }
+                const float v = __fdiv_rn(rg, fn);
+                if (v < bv) {
+                    bv = v;
+                    bcomb = k;
+                }
+            }
+        } else {
+            for (int k = 0; k < ncomb; ++k) {
+                const float v = rg2_of(A.xyz, S, s, nr, [&](int i) {
+                    int kk = k, ci = 0;
+                    for (int j = 0; j <= i; ++j) {
+                        ci = kk % nalt[j];
+                        kk /= nalt[j];
+                    }
+                    return alt_of(A, A.rep_region[r0 + i], ci);
+                });
+                if (v < bv) {
+                    bv = v;
+                    bcomb = k;
+                }
             }
         }
         // the chosen copy of representative i (-1 when no combination was below INF)
@@ -557,9 +755,11 @@ __global__ void __launch_bounds__(kBT) sprite_rg2_kernel(SpriteArgs A) {
             }
             return ci;
         };
+        // the segments with each chromosome's selected copy: the beads from the tables (no
+        // re-read of the selection just stored)
         for (int i = 0; i < ng; ++i)
             A.sel[(size_t)(g0 + i) * S + s] = alt_of(A, A.seg_region[g0 + i], choice(A.seg_rep[g0 + i]));
-        best = rg2_of(A.xyz, S, s, ng, [&](int i) { return A.sel[(size_t)(g0 + i) * S + s]; });
+        best = rg2_regs(A.xyz, S, s, ng, [&](int i) { return alt_of(A, A.seg_region[g0 + i], choice(A.seg_rep[g0 + i])); });
         best = best < kSpriteInf ? best : kSpriteInf;
     }
     A.rg2[(size_t)c * S + s] = best;
@@ -660,21 +860,16 @@ __global__ void __launch_bounds__(kBT) polymer_kernel(PolymerArgs A) {
         }
     }
     __syncthreads();
+    // the ranks of the distances (block_stable_rank)
+    const int npad = pow2_at_least(S);
+    float* sk = reinterpret_cast<float*>(cnt + nb);
+    int* si = reinterpret_cast<int*>(sk + npad);
+    int* rk = si + npad;
+    block_stable_rank(d, S, npad, sk, si, rk);
     const size_t row = (size_t)q * S;
     for (int s = t; s < S; s += kBT) {
         const float ds = d[s];
-        int r = 0, k = 0;
-        for (; k + 4 <= S; k += 4) {
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const float e = d[k + w];
-                r += (e < ds) | ((e == ds) & (k + w < s));
-            }
-        }
-        for (; k < S; ++k) {
-            const float e = d[k];
-            r += (e < ds) | ((e == ds) & (k < s));
-        }
+        const int r = rk[s];
         int lo = 0, hi = nb - 1;  // first value position whose prefix count exceeds r
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -834,7 +1029,7 @@ extern "C" int igm_fish_assign(igm_ctx* c, uint32_t flags, const float* xyz, int
     if (nbead <= 0 || nstruct <= 0 || nhap <= 0 || nitems < 0 || !xyz || !copy_ptr || !copy_idx ||
         (kind != 0 && kind != 1) || (nitems > 0 && !items) || (out_min && !target_min) || (out_max && !target_max))
         return fail(c, IGM_E_INVALID, "igm_fish_assign: invalid arguments");
-    const size_t lds = (size_t)2 * nstruct * sizeof(float);
+    const size_t lds = fish_lds(nstruct);
     if (lds > (size_t)160 * 1024 - 1024)
         return fail(c, IGM_E_UNSUPPORTED, "igm_fish_assign: %d structures exceed the LDS-resident rank kernel",
                     nstruct);
@@ -870,6 +1065,9 @@ extern "C" int igm_fish_assign(igm_ctx* c, uint32_t flags, const float* xyz, int
     FishArgs A{d_xyz, nstruct, d_cptr, d_cidx, kind, d_items, nitems, d_tmin, d_tmax, d_omin, d_omax, d_dmin, d_dmax};
     {
         Timed tm(c, "fish");
+        if (lds > 65536)
+            IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)fish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)lds));
         hipLaunchKernelGGL(fish_kernel, dim3((unsigned)nitems), dim3(kBT), lds, c->stream, A);
         IGM_HIP_CHECK(c, hipGetLastError());
     }
@@ -965,6 +1163,53 @@ extern "C" int igm_sprite_assign(igm_ctx* c, uint32_t flags, const float* xyz, i
     A.alt_bead = d_ab;
     A.rg2 = (float*)p_rg;
     A.sel = (int*)p_sel;
+    {  // the flat bead tables of the clusters whose regions have 1 or 2 copies
+        const char* et = getenv("IGM_SPRITE_TABLES");  // 0: the per-bead index path for every cluster (tests)
+        const bool no_tables = et && atoi(et) == 0;
+        std::vector<int> nc2(ncluster);
+        std::vector<int2> sb2(nseg > 0 ? nseg : 1), rb2(nrep > 0 ? nrep : 1);
+        std::vector<unsigned char> sbit(nseg > 0 ? nseg : 1), rbit(nrep > 0 ? nrep : 1);
+        auto b2 = [&](int rg) {
+            const int a0 = alt_ptr[rg], na = alt_ptr[rg + 1] - a0;
+            return make_int2(alt_bead[a0], alt_bead[a0 + (na > 1 ? 1 : 0)]);
+        };
+        auto ncopy = [&](int rg) { return alt_ptr[rg + 1] - alt_ptr[rg]; };
+        for (int q = 0; q < ncluster; ++q) {
+            const int g0 = seg_ptr[q], ng = seg_ptr[q + 1] - g0, r0 = rep_ptr[q], nr = rep_ptr[q + 1] - r0;
+            bool ok = true;
+            int b = 0;
+            for (int i = 0; i < nr; ++i) {
+                const int rg = rep_region[r0 + i];
+                ok = ok && ncopy(rg) <= 2;
+                rb2[r0 + i] = b2(rg);
+                rbit[r0 + i] = (unsigned char)(ncopy(rg) == 2 ? b : 0);
+                b += ncopy(rg) == 2 ? 1 : 0;
+            }
+            for (int i = 0; i < ng; ++i) {
+                const int rg = seg_region[g0 + i];
+                ok = ok && ncopy(rg) <= 2;
+                sb2[g0 + i] = b2(rg);
+                sbit[g0 + i] = nr > 0 ? rbit[r0 + seg_rep[g0 + i]] : 0;
+            }
+            nc2[q] = ok && !no_tables ? 1 << b : 0;
+        }
+        const int* d_nc2;
+        const int2 *d_sb2, *d_rb2;
+        const unsigned char *d_sbit, *d_rbit;
+        // host-built, so copied whatever IGM_DEVICE_PTRS says about the caller's arrays
+        const uint32_t hf = flags & ~(uint32_t)IGM_DEVICE_PTRS;
+        IGM_TRY(to_device(c, hf, "sp_nc2", nc2.data(), nc2.size(), &d_nc2));
+        IGM_TRY(to_device(c, hf, "sp_sb2", sb2.data(), sb2.size(), &d_sb2));
+        IGM_TRY(to_device(c, hf, "sp_sbit", sbit.data(), sbit.size(), &d_sbit));
+        IGM_TRY(to_device(c, hf, "sp_rb2", rb2.data(), rb2.size(), &d_rb2));
+        IGM_TRY(to_device(c, hf, "sp_rbit", rbit.data(), rbit.size(), &d_rbit));
+        IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));  // (the host tables are freed at the end of this scope)
+        A.ncomb2 = d_nc2;
+        A.seg_b2 = d_sb2;
+        A.seg_bit = d_sbit;
+        A.rep_b2 = d_rb2;
+        A.rep_bit = d_rbit;
+    }
     if ((int64_t)ncluster * A.nsb > 0x7fffffff) return fail(c, IGM_E_UNSUPPORTED, "igm_sprite_assign: grid too large");
     int32_t *d_bi = nullptr, *d_bs = nullptr;
     float* d_bv = nullptr;
@@ -999,7 +1244,8 @@ extern "C" int igm_polymer_assign(igm_ctx* c, uint32_t flags, const float* xyz, 
     if (nbead < 2 || nstruct <= 0 || nloci < 0 || nbins <= 0 || !xyz || !edges || !prob ||
         (nloci > 0 && (!loci || !uniforms || !nn_dist)))
         return fail(c, IGM_E_INVALID, "igm_polymer_assign: invalid arguments");
-    const size_t lds = (size_t)nstruct * sizeof(float) + (size_t)nbins * sizeof(int);
+    const size_t lds = (size_t)nstruct * sizeof(float) + (size_t)nbins * sizeof(int) +
+                       (size_t)2 * pow2_at_least(nstruct) * sizeof(float) + (size_t)nstruct * sizeof(int);
     if (lds > (size_t)160 * 1024 - 1024)
         return fail(c, IGM_E_UNSUPPORTED, "igm_polymer_assign: %d structures x %d bins exceed the LDS-resident kernel",
                     nstruct, nbins);

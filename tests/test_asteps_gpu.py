@@ -235,6 +235,22 @@ def test_sprite_golden_rg2_and_selection(pop):
         assert np.array_equal(got, g['selected'][:, g0:g1][bi2[c]]), c
 
 
+def test_sprite_table_path_equals_index_path(pop, monkeypatch):
+    """The kernel's table path (bead ids of every segment and representative copy in flat
+    host-built tables, representatives' copies in registers) and its per-bead index path
+    (IGM_SPRITE_TABLES=0) give the same bits: Rg^2 of every (cluster, structure), kept
+    structures and selected beads."""
+    from igm_amd import sprite
+    g = load_golden('sprite_cluster_golden.npz')
+    cl, t = golden_tables(pop, g)
+    out = []
+    for mode in ('1', '0'):
+        monkeypatch.setenv('IGM_SPRITE_TABLES', mode)
+        out.append(sprite.rg2_select(pop['coordinates'], pop['copy_ptr'], pop['copy_idx'], t, 5, return_rg2=True))
+    for a, b in zip(*out):
+        assert np.array_equal(bits(a) if a.dtype == np.float32 else a, bits(b) if b.dtype == np.float32 else b)
+
+
 def test_sprite_task_skip_and_errors(pop):
     from igm_amd import sprite
     hc = pop['hap_chrom']
