@@ -1,4 +1,4 @@
-"""bench_issue.json entry from the SQ counter passes of scripts/gpu_r02.sh:
+"""bench_issue.json entry from the SQ pass of scripts/gpu_prof.sh (sum/sq_timed.txt, sq_last.py format):
     python scripts/make_issue.py profiles/<tag> [config B]
 VALU-issue fraction of the SIMDs over the launch: a wave64 VALU instruction occupies
 its SIMD-32 for 2 cycles (MI355X_MICROARCH.md "Wave scheduling"; 4 is the issue cost of

@@ -1,5 +1,5 @@
 """SQ counters of the LAST dispatch of a kernel (the bench's timed launch, after the warmup
-launch) from a rocprofv3 --pmc database, one line per counter in sq_show.py's format:
+launch) from a rocprofv3 --pmc database, one line per counter (kernel, dispatch, counter, instances, value):
     python scripts/sq_last.py <dir> [kernel pattern] > profiles/<tag>/sq_timed.txt"""
 import glob
 import sqlite3
