@@ -1361,6 +1361,10 @@ constexpr bool kPopFused = IGM_POP_FUSED != 0;
 #define IGM_POP_OUTER_CAP 80
 #endif
 constexpr int kPopOuterCap = IGM_POP_OUTER_CAP;  // outer-list entries per slot (two-level lists)
+#ifndef IGM_POP_QX
+#define IGM_POP_QX 2
+#endif
+constexpr int kPopQx = IGM_POP_QX;  // x cells of the build grid per cut_list (pop_fill_slot)
 constexpr int kPopListRow = kPopRowCap + 2;  // u16 per LDS list row of the build (odd word stride)
 // index of cell (cx, cy, cz) in the slot order of a grid of nb[3] cells: x-fastest.
 // (Measured on config C, pop=1000: bricks of 2^3 or 4^3 cells -- 64 or 256 consecutive
@@ -1389,13 +1393,15 @@ __device__ __forceinline__ int pop_cell_index(float x, float y, float z, const f
     pop_cell_xyz(x, y, z, lo, inv, nb, cx, cy, cz);
     return pop_cell_of(cx, cy, cz, nb);
 }
-// The slot runs of the 27 cells around (cx, cy, cz): per (y, z) row the x-run of up to
-// 3 cells, one contiguous slot range (rows outside the grid are empty).  cell[] holds
-// the first slot of every cell (and the end of the last one).
+// The slot runs of the cells around (cx, cy, cz) that can hold a slot within cut_list:
+// per (y, z) row of the 3 x 3 rows the x-run of cells cx - reach .. cx + reach (nb[3]:
+// the x cells span cut_list / qx, so reach <= qx), one contiguous slot range (rows
+// outside the grid are empty).  cell[] holds the first slot of every cell (and the end
+// of the last one).
 __device__ __forceinline__ void pop_runs(int cx, int cy, int cz, const int* cell, const int* nb, int (&rb)[9],
                                          int (&re)[9]) {
-    const int nx = nb[0], ny = nb[1], nz = nb[2];
-    const int xlo = cx > 0 ? cx - 1 : 0, xhi = cx + 1 < nx ? cx + 1 : nx - 1;
+    const int nx = nb[0], ny = nb[1], nz = nb[2], R = nb[3];
+    const int xlo = cx > R ? cx - R : 0, xhi = cx + R < nx ? cx + R : nx - 1;
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
         const int z0 = cz + r / 3 - 1, y0 = cy + r % 3 - 1;
@@ -1433,7 +1439,8 @@ struct PopArgs {
     int* cell;           // (B, kPopCells) first slot of every cell of the build grid
     int ccap;            // cells per grid of this run (<= kPopCellCap; pop_sort_cells)
     float* gp;           // (B, 8) grid lo[3], inv[3]
-    int* gn;             // (B, 8) grid nb[3]
+    int* gn;             // (B, 8) grid nb[3], x reach in cells of cut_list
+    int qx;              // x cells per cut_list: x cells of >= cut_list / qx (runs reach gn[3] x cells each way)
     // bonds of a slot, by buffer parity (as the state): partner slot | type << 16 | lower << 31
     uint32_t* bentb[2];  // (B, nslice, bdmax, 64)
     uint16_t* bdegb[2];  // (B, ldn)
@@ -1721,17 +1728,22 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
             if (!(ext[d] >= 0.0f)) ext[d] = 0.0f;
             vol *= fmaxf(ext[d], cut);
         }
+        // cells of side cs >= cut_list in y and z, cs / qx in x (the sort order is
+        // x-fastest, so an x run of cells stays one slot range, and a slot's list build
+        // visits only the x cells its cut_list sphere meets in each row)
         float cs = cut;
-        const float cap = (float)A.ccap;
-        if (vol / (cs * cs * cs) > cap) cs = cbrtf(vol / cap) * 1.0001f;
+        const float cap = (float)A.ccap, qx = (float)A.qx;
+        if (vol * qx / (cs * cs * cs) > cap) cs = cbrtf(vol * qx / cap) * 1.0001f;
         float* gp = A.gp + (size_t)s * 8;
         int* gn = A.gn + (size_t)s * 8;
         int nbv[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            nbv[d] = (int)floorf(ext[d] / cs);
+            nbv[d] = (int)floorf(d == 0 ? ext[d] * qx / cs : ext[d] / cs);
             if (nbv[d] < 1) nbv[d] = 1;
         }
+        // x cells a pair within cut_list can be apart (the cell walk's x reach)
+        gn[3] = ext[0] > 0.0f ? max(1, (int)ceilf(cut * (float)nbv[0] / ext[0] * 1.00001f)) : 1;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             const int nbd = nbv[d];
@@ -1994,13 +2006,6 @@ __device__ __forceinline__ float4 pop_ld(__amdgpu_buffer_rsrc_t r, uint32_t j) {
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 
-// Verlet list of every bead slot of a flagged structure: the 27 cells around its cell,
-// each x-run of cells one contiguous slot range.  Measured on config C (kernel traces,
-// scripts/gpu_profab.sh): collecting the list in an LDS row and storing it a quad at a
-// time is 13 % faster than one global u16 store per entry; batches of 4 slots per run
-// beat 2 and 6.  Staging positions in LDS does not pay, neither the block's whole
-// neighbourhood range (~50 KB, 18 % slower) nor the union of the slots its lists use
-// (lists rewritten to union indices: this kernel +58 %, the force kernel +9 %).
 // The Verlet list of bead slot i of structure s (p0 its position): collected in the
 // thread's LDS row `row` (kPopListRow u16), padded to whole quads with the slot itself,
 // stored as quads to the global list and its length (or kNnbWalk) to nnb.  Returns
@@ -2034,7 +2039,8 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
             kr -= flush_at;
         }
     };
-    // The 27 cells are 9 x-runs of slots.  All 18 run bounds are loaded together,
+    // The 3 x 3 rows' x-runs of cells (cx - reach .. cx + reach, pop_runs) are 9 slot
+    // ranges.  All 18 run bounds are loaded together,
     // then each z-layer's 3 runs a batch of kFillW slots per run at once, the rest of a
     // longer run kFillTail slots at a time (the hot runs' lists reach 3.4 rmax: ~10
     // candidates per run; one dependent load per candidate there was +2 % anneal).
@@ -3640,6 +3646,28 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     IGM_HIP_CHECK(c, hipStreamSynchronize(c->stream));
     if (dmax > 0xFFFF) return fail(c, IGM_E_UNSUPPORTED, "an atom has %d bonds", dmax);
     Q.bdmax = dmax > 0 ? dmax : 1;
+    Q.kq = ((pr.P.kcap == kNeighBudget ? kPopListCap : std::min(pr.P.kcap, kPopListCap)) + 3) / 4;
+    {
+        // HBM of the engine's state, per slot: two parity buffers of (position 16, velocity
+        // 12, force 12, atom id 4, slot 4, flags 1), build position 12, Verlet list 8 kq (512
+        // B at the default 256 entries -- most of it), list length 2, bonds 2 x 4 bdmax, degree
+        // 2 x 2, slot remaps 8; per structure the cell offsets.  At config C (1000 x 29 839
+        // slots) the lists alone are 15.3 GB.  Checked against the free HBM (plus what this
+        // context's population workspace already holds) before anything is allocated.
+        const size_t per_slot = 2 * (16 + 12 + 12 + 4 + 4 + 1) + 12 + 8 * (size_t)Q.kq + 2 + 8 * (size_t)Q.bdmax + 4 + 8;
+        const size_t need = per_slot * SL + sizeof(int) * (size_t)S * kPopCells;
+        size_t held = 0;
+        for (const auto& kv : c->ws)
+            if (kv.first.compare(0, 4, "pop_") == 0) held += kv.second.second;
+        size_t fre = 0, tot = 0;
+        if (hipMemGetInfo(&fre, &tot) == hipSuccess && need > fre + held)
+            return fail(c, IGM_E_NOMEM,
+                        "population engine: %zu structures x %d slots need %.1f GB of HBM (%.1f MB per structure, "
+                        "%.1f of it the %d-entry Verlet lists), %.1f GB free: pass fewer structures per call or a "
+                        "smaller neigh_capacity", (size_t)S, ldn, need / 1e9, need / 1e6 / S,
+                        8.0 * Q.kq * ldn / 1e6, 4 * Q.kq, (fre + held) / 1e9);
+        (void)hipGetLastError();
+    }
     for (int b = 0; b < 2; ++b) {
         char nm[6][16];
         const char* what[6] = {"pos", "vel", "frc", "aid", "slot", "flg"};
@@ -3654,9 +3682,8 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     void *ppar, *pxb, *pnl, *pnnb, *pcell, *pgp, *pgn, *pbent, *pbdeg, *pfl, *pfli, *pnf, *pke, *pbb;
     IGM_TRY(workspace(c, "pop_par", sizeof(int) * S, &ppar));
     IGM_TRY(workspace(c, "pop_xb", sizeof(pop_f3) * SL, &pxb));
-    // the list capacity: kPopListCap, or a smaller neigh_capacity given in the params (the
-    // default 64 is the LDS engine's budget)
-    Q.kq = ((pr.P.kcap == kNeighBudget ? kPopListCap : std::min(pr.P.kcap, kPopListCap)) + 3) / 4;
+    // (Q.kq above: the list capacity, kPopListCap or a smaller neigh_capacity given in the
+    // params -- the default 64 is the LDS engine's budget)
     IGM_TRY(workspace(c, "pop_nl", sizeof(uint2) * SL * Q.kq, &pnl));
     IGM_TRY(workspace(c, "pop_nnb", sizeof(uint16_t) * SL, &pnnb));
     IGM_TRY(workspace(c, "pop_cell", sizeof(int) * (size_t)S * kPopCells, &pcell));
@@ -3780,6 +3807,10 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     }
     // the sort keeps its ids in LDS when they fit beside the cell counts (200 kb: 29 839 atoms)
     Q.ccap = pop_sort_cells(N);
+    {  // x cells per cell side (IGM_POP_QX: A/B only)
+        const char* e = getenv("IGM_POP_QX");
+        Q.qx = e ? std::max(1, std::min(4, atoi(e))) : kPopQx;
+    }
     const bool ids_lds = pop_sort_lds(true, N, Q.ccap) <= kLdsBytes;
     const size_t sort_lds = pop_sort_lds(ids_lds, N, Q.ccap);
     auto sort_kern = !ids_lds ? pop_sort_kernel<false, 0>

@@ -282,7 +282,10 @@ typedef struct {
     int32_t neigh_capacity; /* HBM neighbour-list budget, mean entries per atom (0 = 64); atoms past
                                the budget take their pair forces from a walk of the build-time cell grid.
                                The population engine (structures too large for LDS) lists up to 256
-                               entries per atom when this is 0 or 64, else min(this, 256) */
+                               entries per atom when this is 0 or 64, else min(this, 256); its
+                               HBM is ~(120 + 2 x entries + 8 x max bond degree) B per atom per
+                               structure (the 256-entry lists alone 15.3 GB for 1000 x 29 839 atoms), checked against the free
+                               HBM before the run (IGM_E_NOMEM names the per-structure cost) */
     int32_t flags;          /* IGM_MSTEP_* below                        */
     int32_t env_kind[IGM_MAX_ENVELOPES]; /* IGM_ENV_ELLIPSOID (0) or IGM_ENV_VOLUME (1)  */
 } igm_mstep_params;
