@@ -1361,6 +1361,10 @@ constexpr bool kPopFused = IGM_POP_FUSED != 0;
 #define IGM_POP_OUTER_CAP 80
 #endif
 constexpr int kPopOuterCap = IGM_POP_OUTER_CAP;  // outer-list entries per slot (two-level lists)
+#ifndef IGM_POP_TYPE_STAGE
+#define IGM_POP_TYPE_STAGE 512  // bond types a force block stages in LDS (4 KB); 0: always gathered
+#endif
+constexpr int kPopTypeStage = IGM_POP_TYPE_STAGE > 0 ? IGM_POP_TYPE_STAGE : 1;
 #ifndef IGM_POP_QX
 #define IGM_POP_QX 2
 #endif
@@ -2231,7 +2235,8 @@ __device__ __noinline__ float4 pop_walk_pairs(const float4* pos, const int* cell
 // following steps) and used directly.
 __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, size_t base, const float4* pos,
                                                uint32_t fl, float evf, float envf, float& fx, float& fy,
-                                               float& fz, const uint32_t* lrow = nullptr, int nn_built = 0) {
+                                               float& fz, const IGM_LDS float2* sbt, bool lds_types,
+                                               const uint32_t* lrow = nullptr, int nn_built = 0) {
     constexpr int U = kPopPairBatch;  // list quads per batch
     const int nsl = A.cm.nslice;
     const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
@@ -2392,7 +2397,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             pt[u] = pop_ld(rp, et[u] & 0xffffu);
-            ct[u] = bt[(et[u] >> 16) & 0x7fffu];
+            ct[u] = lds_types ? sbt[(et[u] >> 16) & 0x7fffu] : bt[(et[u] >> 16) & 0x7fffu];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) bond(pt[u], ct[u], et[u], k0 + u < deg);
@@ -2459,6 +2464,16 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
     }
     const size_t base = (size_t)s * A.cm.ldn, k = base + i;
     const PopBuf& B = A.buf[A.par[s]];
+    // the structure's bond types (r0, k) staged in LDS when they fit: a bond's type is then an
+    // LDS read, not one more gather through the texture path (which bounds this kernel)
+    __shared__ float2 sbt[kPopTypeStage];
+    const int64_t ntyp = A.cm.bonds.ntype[s];
+    const bool lds_types = IGM_POP_TYPE_STAGE > 0 && ntyp <= kPopTypeStage;
+    if (lds_types) {
+        const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
+        for (int q = threadIdx.x; q < (int)ntyp; q += kPopBS) sbt[q] = bt[q];
+    }
+    __syncthreads();
     double ke = 0.0;
     if (i < A.cm.natom) {
         pop_f3 v = B.vel[k];
@@ -2473,9 +2488,9 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
                                           kPopListRow - 2);
             else
                 A.nnb[k] = 0;
-            pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, row, nb);
+            pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, (const IGM_LDS float2*)sbt, lds_types, row, nb);
         } else {
-            pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz);
+            pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, (const IGM_LDS float2*)sbt, lds_types);
         }
         B.frc[k] = pop_f3{fx, fy, fz};
         if (S.integrate && !(fl & IGM_ATOM_FIXED)) {
