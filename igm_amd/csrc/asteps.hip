@@ -85,6 +85,114 @@ __device__ void block_stable_rank(const float* v, int n, int npad, float* sk, in
     __syncthreads();
 }
 
+// block_stable_rank for npad = E * kBT (E <= 8): thread t holds the E consecutive keys
+// t E .. t E + E - 1 in registers as u64 (the value's order-preserving bits above its index,
+// so equal values order by index -- the same stable order as above).  A bitonic stage with partner distance j < E
+// swaps inside a thread, E <= j < 64 E exchanges through a wave shuffle, and only the
+// stages with j >= 64 E (3 of the 55 at npad = 1024) go through LDS (hi and lo words in the
+// sk / si arrays) with a barrier.
+template <int E, int C>
+__device__ void block_stable_rank_reg(const float* const (&v)[C], int n, uint32_t* kh, uint32_t* kl,
+                                      int* const (&rank)[C]) {
+    const int t = threadIdx.x;
+    constexpr int NP = E * kBT;
+    uint64_t key[C][E];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int p = t * E + e;
+            // IEEE bits made order-preserving for every sign (negative: all bits flipped); the
+            // pad is +inf with an index >= n.  (-0 would sort before +0 where the float compare
+            // ties them: the columns ranked here are norms, never -0.)
+            const uint32_t bits = p < n ? __float_as_uint(v[c][p]) : 0x7f800000u;
+            const uint32_t ord = bits ^ ((bits >> 31) ? 0xffffffffu : 0x80000000u);
+            key[c][e] = ((uint64_t)ord << 32) | (uint32_t)p;
+        }
+#pragma unroll
+    for (int k = 2; k <= NP; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j < E) {
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int e = 0; e < E; ++e)
+                        if ((e & j) == 0) {
+                            const int p = t * E + e;
+                            const uint64_t a = key[c][e], b = key[c][e | j];
+                            const bool up = (p & k) == 0;
+                            key[c][e] = up ? (a < b ? a : b) : (a < b ? b : a);
+                            key[c][e | j] = up ? (a < b ? b : a) : (a < b ? a : b);
+                        }
+            } else {
+                uint64_t o[C][E];
+                if (j < 64 * E) {
+                    const int d = j / E;  // lane distance of the partner
+#pragma unroll
+                    for (int c = 0; c < C; ++c)
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const uint32_t h = __shfl_xor((int)(uint32_t)(key[c][e] >> 32), d, 64),
+                                           l = __shfl_xor((int)(uint32_t)key[c][e], d, 64);
+                            o[c][e] = ((uint64_t)h << 32) | l;
+                        }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < C; ++c)
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            kh[c * NP + t * E + e] = (uint32_t)(key[c][e] >> 32);
+                            kl[c * NP + t * E + e] = (uint32_t)key[c][e];
+                        }
+                    __syncthreads();
+#pragma unroll
+                    for (int c = 0; c < C; ++c)
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const int q = c * NP + ((t * E + e) ^ j);
+                            o[c][e] = ((uint64_t)kh[q] << 32) | kl[q];
+                        }
+                    __syncthreads();
+                }
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int p = t * E + e;
+                        const bool up = (p & k) == 0, lower = (p & j) == 0;
+                        const uint64_t a = key[c][e], b = o[c][e];
+                        key[c][e] = (up == lower) ? (a < b ? a : b) : (a < b ? b : a);
+                    }
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int p = t * E + e;
+            if (p < n) rank[c][(uint32_t)key[c][e]] = p;
+        }
+    __syncthreads();
+}
+
+// the stable ranks of C columns v[c][0..n): the register sort (all C columns through one
+// network) when npad = E kBT, E <= 8, else the LDS sort column by column.  Scratch: sk and
+// si of C npad words each.
+template <int C>
+__device__ void stable_rank(const float* const (&v)[C], int n, int npad, float* sk, int* si, int* const (&rank)[C]) {
+    __syncthreads();  // (v complete)
+    uint32_t* kh = reinterpret_cast<uint32_t*>(sk);
+    uint32_t* kl = reinterpret_cast<uint32_t*>(si);
+    if (npad == kBT) block_stable_rank_reg<1, C>(v, n, kh, kl, rank);
+    else if (npad == 2 * kBT) block_stable_rank_reg<2, C>(v, n, kh, kl, rank);
+    else if (npad == 4 * kBT) block_stable_rank_reg<4, C>(v, n, kh, kl, rank);
+    else if (npad == 8 * kBT) block_stable_rank_reg<8, C>(v, n, kh, kl, rank);
+    else
+        for (int c = 0; c < C; ++c) block_stable_rank(v[c], n, npad, sk, si, rank[c]);
+}
+
 __host__ __device__ inline int pow2_at_least(int n) {
     int p = 1;
     while (p < n) p <<= 1;
@@ -459,11 +567,12 @@ __global__ void __launch_bounds__(kBT) fish_kernel(FishArgs A) {
     // the ranks of the column (block_stable_rank), min then max
     const int npad = pow2_at_least(S);
     float* sk = fsm + 2 * S;
-    int* si = reinterpret_cast<int*>(sk + npad);
-    int* rmin = si + npad;
+    int* si = reinterpret_cast<int*>(sk + 2 * npad);
+    int* rmin = si + 2 * npad;
     int* rmax = rmin + S;
-    block_stable_rank(vmin, S, npad, sk, si, rmin);
-    block_stable_rank(vmax, S, npad, sk, si, rmax);
+    const float* const cols[2] = {vmin, vmax};
+    int* const ranks[2] = {rmin, rmax};
+    stable_rank<2>(cols, S, npad, sk, si, ranks);
     const size_t row = (size_t)q * S;
     for (int s = threadIdx.x; s < S; s += kBT) {
         if (A.omin) A.omin[row + s] = A.tmin[row + rmin[s]];
@@ -473,8 +582,8 @@ __global__ void __launch_bounds__(kBT) fish_kernel(FishArgs A) {
     }
 }
 
-// LDS of fish_kernel: the min and max columns, the sort's keys and indices, two rank columns
-inline size_t fish_lds(int S) { return sizeof(float) * (4 * (size_t)S + 2 * (size_t)pow2_at_least(S)); }
+// LDS of fish_kernel: the min and max columns, the sort's keys and indices (both columns), two rank columns
+inline size_t fish_lds(int S) { return sizeof(float) * (4 * (size_t)S + 4 * (size_t)pow2_at_least(S)); }
 
 // ============================================================================ SPRITE
 struct SpriteArgs {
@@ -767,11 +876,45 @@ __global__ void __launch_bounds__(kBT) sprite_rg2_kernel(SpriteArgs A) {
 
 // keep_best (SpriteAssignmentStep.py:138-143): the keep_best smallest Rg^2 of a
 // cluster in increasing order (ties by structure index), their values and the
-// selected beads of those structures, row-major (keep_best, len(cluster)).
+// selected beads of those structures, row-major (keep_best, len(cluster)).  The rank of
+// every structure comes from the block's stable sort of the column (stable_rank), where
+// counting each rank against the whole column was O(S^2) per cluster (7.7 of the 11 ms
+// of config D/E's SPRITE step).
 __global__ void __launch_bounds__(kBT) sprite_keep_best_kernel(const float* __restrict__ rg2, const int* __restrict__ sel,
                                                                const int* __restrict__ seg_ptr, int S, int kb,
                                                                int* __restrict__ best_idx, float* __restrict__ best_val,
                                                                int* __restrict__ best_sel) {
+    extern __shared__ float ksm[];
+    const int c = blockIdx.x;
+    const int npad = pow2_at_least(S);
+    float* sk = ksm + S;
+    int* si = reinterpret_cast<int*>(sk + npad);
+    int* rk = si + npad;
+    const float* v = rg2 + (size_t)c * S;
+    for (int s = threadIdx.x; s < S; s += kBT) ksm[s] = v[s];
+    const float* const cols[1] = {ksm};
+    int* const ranks[1] = {rk};
+    stable_rank<1>(cols, S, npad, sk, si, ranks);
+    const int g0 = seg_ptr[c], ng = seg_ptr[c + 1] - g0;
+    for (int s = threadIdx.x; s < S; s += kBT) {
+        const int r = rk[s];
+        if (r < kb) {
+            best_idx[(size_t)c * kb + r] = s;
+            best_val[(size_t)c * kb + r] = ksm[s];
+            int* out = best_sel + (size_t)g0 * kb + (size_t)r * ng;
+            for (int i = 0; i < ng; ++i) out[i] = sel[(size_t)(g0 + i) * S + s];
+        }
+    }
+}
+
+// keep_best by counting every rank against the column: the fallback for populations
+// whose sort scratch does not fit (S > ~9 000), LDS of the column only
+__global__ void __launch_bounds__(kBT) sprite_keep_best_count_kernel(const float* __restrict__ rg2,
+                                                                     const int* __restrict__ sel,
+                                                                     const int* __restrict__ seg_ptr, int S, int kb,
+                                                                     int* __restrict__ best_idx,
+                                                                     float* __restrict__ best_val,
+                                                                     int* __restrict__ best_sel) {
     extern __shared__ float ksm[];
     const int c = blockIdx.x;
     const float* v = rg2 + (size_t)c * S;
@@ -793,6 +936,10 @@ __global__ void __launch_bounds__(kBT) sprite_keep_best_kernel(const float* __re
         }
     }
 }
+
+// LDS of sprite_keep_best_kernel: the column, the sort's keys and indices, the ranks
+constexpr size_t kSortLdsMax = (size_t)160 * 1024 - 1024;  // one CU's LDS, less the static part
+inline size_t keep_best_lds(int S) { return sizeof(float) * (2 * (size_t)S + 2 * (size_t)pow2_at_least(S)); }
 
 // ============================================================================ polymer
 // PolymerAssignmentStep.task (igm/steps/PolymerAssignmentStep.py:84-129): for locus i,
@@ -865,7 +1012,9 @@ __global__ void __launch_bounds__(kBT) polymer_kernel(PolymerArgs A) {
     float* sk = reinterpret_cast<float*>(cnt + nb);
     int* si = reinterpret_cast<int*>(sk + npad);
     int* rk = si + npad;
-    block_stable_rank(d, S, npad, sk, si, rk);
+    const float* const cols[1] = {d};
+    int* const ranks[1] = {rk};
+    stable_rank<1>(cols, S, npad, sk, si, ranks);
     const size_t row = (size_t)q * S;
     for (int s = t; s < S; s += kBT) {
         const float ds = d[s];
@@ -1222,9 +1371,18 @@ extern "C" int igm_sprite_assign(igm_ctx* c, uint32_t flags, const float* xyz, i
         hipLaunchKernelGGL(sprite_rg2_kernel, dim3((unsigned)(ncluster * A.nsb)), dim3(kBT), 0, c->stream, A);
         IGM_HIP_CHECK(c, hipGetLastError());
         if (keep_best > 0) {
-            hipLaunchKernelGGL(sprite_keep_best_kernel, dim3((unsigned)ncluster), dim3(kBT),
-                               (size_t)nstruct * sizeof(float), c->stream, (const float*)p_rg, (const int*)p_sel, d_sp,
-                               nstruct, keep_best, d_bi, d_bv, d_bs);
+            const size_t klds = keep_best_lds(nstruct);
+            if (klds <= kSortLdsMax) {
+                if (klds > 65536)
+                    IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)sprite_keep_best_kernel,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)klds));
+                hipLaunchKernelGGL(sprite_keep_best_kernel, dim3((unsigned)ncluster), dim3(kBT), klds, c->stream,
+                                   (const float*)p_rg, (const int*)p_sel, d_sp, nstruct, keep_best, d_bi, d_bv, d_bs);
+            } else {
+                hipLaunchKernelGGL(sprite_keep_best_count_kernel, dim3((unsigned)ncluster), dim3(kBT),
+                                   (size_t)nstruct * sizeof(float), c->stream, (const float*)p_rg, (const int*)p_sel,
+                                   d_sp, nstruct, keep_best, d_bi, d_bv, d_bs);
+            }
             IGM_HIP_CHECK(c, hipGetLastError());
         }
     }

@@ -186,6 +186,25 @@ def test_fish_task_dict_and_ties(pop):
     assert np.array_equal(omin[0], t[0])
 
 
+@pytest.mark.parametrize('S', [50, 200, 256, 300, 512, 700, 1024, 1500, 2048, 2100])
+def test_fish_rank_widths_with_ties(S):
+    """The rank sort at every width it takes (registers for npad = 256, 512, 1024, 2048;
+    LDS otherwise): radial distances rounded to a few values, so most ranks are decided by
+    structure order, against the oracle's argsort(argsort(kind='stable'))."""
+    from igm_amd import fish
+    rng = np.random.default_rng(S)
+    xyz = np.round(rng.normal(0.0, 2.0, (4, S, 3))).astype(np.float32)  # integer lattice: many equal norms
+    cptr = np.array([0, 2, 3], np.int32)
+    cidx = np.array([0, 1, 2], np.int32)
+    probes = np.array([0, 1], np.int32)
+    tmin = np.sort(rng.random((2, S)), axis=1).astype(np.float32)
+    tmax = np.sort(rng.random((2, S)), axis=1).astype(np.float32)
+    omin, omax = fish.assign(xyz, cptr, cidx, 'probe', probes, tmin, tmax)
+    rmin, rmax, _, _ = A.fish_radial(xyz, cptr, cidx, probes, tmin, tmax)
+    assert np.array_equal(bits(omin), bits(rmin))
+    assert np.array_equal(bits(omax), bits(rmax))
+
+
 def test_fish_full_size_200kb(pop200):
     from igm_amd import fish, synthetic
     p = pop200
@@ -264,6 +283,28 @@ def test_sprite_task_skip_and_errors(pop):
     with pytest.raises(RuntimeError):  # keep_best must be < nstruct (np.argpartition)
         sprite.task(pop['coordinates'], clusters, hc, pop['copy_ptr'], pop['copy_idx'],
                     keep_best=pop['coordinates'].shape[1])
+
+
+@pytest.mark.parametrize('S', [50, 256, 700, 1024, 2048, 2100, 9000])
+def test_sprite_keep_best_widths_and_ties(S):
+    """keep_best at every width of the rank sort (and the counting kernel past the sort's
+    LDS, S = 9000): a lattice population where many structures share an Rg^2, so the order
+    of the kept structures is decided by structure index -- a stable argsort of the column."""
+    from igm_amd import sprite
+    rng = np.random.default_rng(S)
+    nbead = 6
+    xyz = np.round(rng.normal(0.0, 1.0, (nbead, S, 3))).astype(np.float32)
+    copy_ptr = np.arange(nbead + 1, dtype=np.int32)
+    copy_idx = np.arange(nbead, dtype=np.int32)
+    chrom = np.zeros(nbead, np.int64)
+    t = sprite.cluster_tables([np.array([0, 1, 2]), np.array([2, 3, 4, 5]), np.array([1, 5])], chrom, copy_ptr)
+    kb = min(50, S - 1)
+    bi, bv, bs, rg2 = sprite.rg2_select(xyz, copy_ptr, copy_idx, t, kb, return_rg2=True)
+    for c in range(3):
+        order = np.argsort(rg2[c], kind='stable')[:kb]
+        assert len(np.unique(rg2[c])) < S  # ties are the point
+        assert np.array_equal(bi[c], order)
+        assert np.array_equal(bits(bv[c]), bits(rg2[c][order]))
 
 
 def test_sprite_full_size_200kb(pop200):
