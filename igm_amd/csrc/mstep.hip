@@ -1366,9 +1366,12 @@ constexpr int kPopOuterCap = IGM_POP_OUTER_CAP;  // outer-list entries per slot 
 #endif
 constexpr int kPopTypeStage = IGM_POP_TYPE_STAGE > 0 ? IGM_POP_TYPE_STAGE : 1;
 #ifndef IGM_POP_QX
-#define IGM_POP_QX 2
+#define IGM_POP_QX 1
 #endif
-constexpr int kPopQx = IGM_POP_QX;  // x cells of the build grid per cut_list (pop_fill_slot)
+// x cells of the build grid per cut_list.  2 (half-width x cells, 5-cell runs) was 1 % faster
+// in one-group kernel traces (fill -1 %, force -1.3 %) but 1 % slower in the bench's two-group
+// anneal (profiles/r05_ab), so cubic cells stay the default.
+constexpr int kPopQx = IGM_POP_QX;
 constexpr int kPopListRow = kPopRowCap + 2;  // u16 per LDS list row of the build (odd word stride)
 // index of cell (cx, cy, cz) in the slot order of a grid of nb[3] cells: x-fastest.
 // (Measured on config C, pop=1000: bricks of 2^3 or 4^3 cells -- 64 or 256 consecutive
