@@ -541,6 +541,50 @@ __global__ void __launch_bounds__(kBT) fish_kernel(FishArgs A) {
         b0 = A.cptr[g];
         nb = A.cptr[g + 1] - b0;
     }
+    if (na <= 2 && nb <= 2 && na > 0 && (A.kind == 0 || nb > 0)) {
+        // <= 2 copies a side (every diploid locus): a thread's U structures and all their
+        // copies' positions are loaded together, one memory round trip (the min / max do
+        // not depend on the order the distances are taken in)
+        constexpr int U = 4;
+        const int ia0 = A.cidx[a0], ia1 = A.cidx[a0 + na - 1];
+        const int ib0 = nb > 0 ? A.cidx[b0] : 0, ib1 = nb > 0 ? A.cidx[b0 + nb - 1] : 0;
+        for (int s0 = threadIdx.x; s0 < S; s0 += U * kBT) {
+            float p[4][U][3];  // copies a0, a1, b0, b1
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int s = min(s0 + u * kBT, S - 1);
+                load3(A.xyz, S, ia0, s, p[0][u][0], p[0][u][1], p[0][u][2]);
+                load3(A.xyz, S, ia1, s, p[1][u][0], p[1][u][1], p[1][u][2]);
+                if (A.kind != 0) {
+                    load3(A.xyz, S, ib0, s, p[2][u][0], p[2][u][1], p[2][u][2]);
+                    load3(A.xyz, S, ib1, s, p[3][u][0], p[3][u][1], p[3][u][2]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int s = s0 + u * kBT;
+                if (s >= S) break;
+                float mn = INFINITY, mx = -INFINITY;
+                auto take = [&](float d) {
+                    mn = d < mn ? d : mn;
+                    mx = d > mx ? d : mx;
+                };
+                if (A.kind == 0) {
+                    take(norm3(p[0][u][0], p[0][u][1], p[0][u][2]));
+                    take(norm3(p[1][u][0], p[1][u][1], p[1][u][2]));
+                } else {
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int b = 2; b < 4; ++b)
+                            take(norm3(__fsub_rn(p[a][u][0], p[b][u][0]), __fsub_rn(p[a][u][1], p[b][u][1]),
+                                       __fsub_rn(p[a][u][2], p[b][u][2])));
+                }
+                vmin[s] = mn;
+                vmax[s] = mx;
+            }
+        }
+    } else
     for (int s = threadIdx.x; s < S; s += kBT) {
         float mn = INFINITY, mx = -INFINITY;
         for (int a = 0; a < na; ++a) {
