@@ -128,7 +128,7 @@ def test_gpu_200kb_full_protocol_stagewise_matches_oracle(heartbeat):
     min cg), on frustrated restraints, compared stage by stage with the fp64 oracle.
 
     A 200 kb population runs one warmup A/M iteration on the GPU (AMIteration); from that
-    state the next iteration's A-step and selection give 16 structures ~34 000 Hi-C bonds
+    state the next iteration's A-step and selection give all 32 structures ~34 000 Hi-C bonds
     each, and 700 random long-range contacts per structure are added on top (restraints that
     cannot all be met: the final energies stay far from zero instead of reaching ~1e-11 per
     bead on the self-consistent synthetic .hcs alone).  Both engines then run the
@@ -140,7 +140,7 @@ def test_gpu_200kb_full_protocol_stagewise_matches_oracle(heartbeat):
     (lammps_io.py:6-37) -- and after the final CG (igm_mstep_run / the oracle with no MD
     stage) the final energies and violation fractions.  Every stage's energies and the final
     state agree by the two-sample KS test of tests/mstep_stats.py and by the paired Wilcoxon
-    signed-rank test over the 16 structures (both at alpha = 1e-3; the pairing removes the
+    signed-rank test over the 32 structures (both at alpha = 1e-3; the pairing removes the
     structure-to-structure spread, so a systematic difference of a few per cent separates
     them); the temperatures, which temp/rescale holds within its window (0.1) of the target,
     differ by at most twice the window.  Everything is recorded in gpurun_out/configC_stagewise.json beside the
@@ -150,7 +150,7 @@ def test_gpu_200kb_full_protocol_stagewise_matches_oracle(heartbeat):
     from igm_amd import mstep
     from igm_amd.pipeline import AMIteration
     from igm_amd._lib import bond_dtype
-    S, n = 32, 16
+    S, n = 32, 32
     pop = syn.population_200kb(S, first_sid=0)
     atoms = M.Atoms(pop['radii'])
     x = np.zeros((S, atoms.n, 3), np.float32)
