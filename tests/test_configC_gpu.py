@@ -128,8 +128,8 @@ def test_gpu_200kb_full_protocol_stagewise_matches_oracle(heartbeat):
     min cg), on frustrated restraints, compared stage by stage with the fp64 oracle.
 
     A 200 kb population runs one warmup A/M iteration on the GPU (AMIteration); from that
-    state the next iteration's A-step and selection give all 32 structures ~34 000 Hi-C bonds
-    each, and 700 random long-range contacts per structure are added on top (restraints that
+    state the next iteration's A-step and selection give 16 (IGM_STAGEWISE_N) structures ~34 000
+    Hi-C bonds each, and 700 random long-range contacts per structure are added on top (restraints that
     cannot all be met: the final energies stay far from zero instead of reaching ~1e-11 per
     bead on the self-consistent synthetic .hcs alone).  Both engines then run the
     protocol's segments from the same coordinates with the same velocities at every
@@ -140,7 +140,7 @@ def test_gpu_200kb_full_protocol_stagewise_matches_oracle(heartbeat):
     (lammps_io.py:6-37) -- and after the final CG (igm_mstep_run / the oracle with no MD
     stage) the final energies and violation fractions.  Every stage's energies and the final
     state agree by the two-sample KS test of tests/mstep_stats.py and by the paired Wilcoxon
-    signed-rank test over the 32 structures (both at alpha = 1e-3; the pairing removes the
+    signed-rank test over the n structures (both at alpha = 1e-3; the pairing removes the
     structure-to-structure spread, so a systematic difference of a few per cent separates
     them); the temperatures, which temp/rescale holds within its window (0.1) of the target,
     differ by at most twice the window.  Everything is recorded in gpurun_out/configC_stagewise.json beside the
@@ -150,7 +150,12 @@ def test_gpu_200kb_full_protocol_stagewise_matches_oracle(heartbeat):
     from igm_amd import mstep
     from igm_amd.pipeline import AMIteration
     from igm_amd._lib import bond_dtype
-    S, n = 32, 32
+    # 16 structures in the suite (the oracle runs one per thread on the box's 16 CPUs: 32 would
+    # double its ~260 s and crowd the round-end GPU tier's 900 s); IGM_STAGEWISE_N=32 for the
+    # recorded 32-structure run (profiles/r05_parity/configC_stagewise.json)
+    S = 32
+    n = int(os.environ.get('IGM_STAGEWISE_N', '16'))
+    assert 2 <= n <= S
     pop = syn.population_200kb(S, first_sid=0)
     atoms = M.Atoms(pop['radii'])
     x = np.zeros((S, atoms.n, 3), np.float32)
