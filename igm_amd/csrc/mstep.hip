@@ -1375,7 +1375,7 @@ constexpr int kPopQx = IGM_POP_QX;
 constexpr int kPopListRow = kPopRowCap + 2;  // u16 per LDS list row of the build (odd word stride)
 // index of cell (cx, cy, cz) in the slot order of a grid of nb[3] cells: x-fastest.
 // (Measured on config C, pop=1000: bricks of 2^3 or 4^3 cells -- 64 or 256 consecutive
-// slots a compact blob instead of a rod along x -- were 12 % and 13 % SLOWER)
+// slots a compact blob instead of a rod along x -- were 12 % and 13 % SLOWER, profiles/history_r01_r04.md.)
 __device__ __forceinline__ int pop_cell_of(int cx, int cy, int cz, const int* nb) {
     return (cz * nb[1] + cy) * nb[0] + cx;
 }
@@ -3995,7 +3995,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
 }
 
 // HBM-size structures: the multi-kernel population engine.  (The domain-decomposed
-// engine of round 3 -- 31.3 s against 16.1 s on config C, DESIGN.md section 7 -- is
+// engine of round 3 -- 31.3 s against 16.1 s on config C, profiles/history_r01_r04.md -- is
 // retired; its params flag 0x4 is rejected.)
 int run_anneal_big(igm_ctx* c, const Prepared& pr, const AnnealArgs& A, int32_t pflags) {
     if (pflags & 0x4) return fail(c, IGM_E_UNSUPPORTED, "the domain-decomposed engine (params flag 0x4) is retired");

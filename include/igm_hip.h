@@ -301,7 +301,7 @@ typedef struct {
                                       (DamID) and active/inactive centroid slots (SPRITE); the
                                       IGM_ATOM_BEAD bit must be the same in every structure */
 /* 0x4 is retired (round 3's domain-decomposed engine, 2x slower than the population engine on
-   the 200 kb model): igm_mstep_run returns IGM_E_UNSUPPORTED for it */
+   the 200 kb model, profiles/history_r01_r04.md): igm_mstep_run returns IGM_E_UNSUPPORTED for it */
 
 /* atom flags (per atom, shared by all structures of a batch) */
 #define IGM_ATOM_BEAD 0x1u   /* takes part in the soft pair potential       */
