@@ -687,7 +687,13 @@ __device__ __forceinline__ float rg2_of(const float* __restrict__ xyz, int S, in
 
 // rg2_of with the n <= kRegBeads positions loaded into registers first (all in flight
 // together, each read once): the same sums in the same order, bit for bit
-constexpr int kRegBeads = 20;
+#ifndef IGM_SPRITE_REG_BEADS
+// segments whose positions the final Rg^2 pass keeps in registers (more: two passes of loads).
+// 12 keeps sprite_rg2_kernel at 86 VGPRs (5 waves per SIMD; 20 needed 146, 3 waves): SPRITE
+// 3.45 ms against 3.95 (200 kb x 1000, 20 000 clusters of <= 20 segments, profiles/r05_de)
+#define IGM_SPRITE_REG_BEADS 12
+#endif
+constexpr int kRegBeads = IGM_SPRITE_REG_BEADS;
 template <class Bead>
 __device__ __forceinline__ float rg2_regs(const float* __restrict__ xyz, int S, int s, int n, Bead bead) {
     if (n > kRegBeads) return rg2_of(xyz, S, s, n, bead);
