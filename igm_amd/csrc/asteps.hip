@@ -689,9 +689,9 @@ __device__ __forceinline__ float rg2_of(const float* __restrict__ xyz, int S, in
 // together, each read once): the same sums in the same order, bit for bit
 #ifndef IGM_SPRITE_REG_BEADS
 // segments whose positions the final Rg^2 pass keeps in registers (more: two passes of loads).
-// 12 keeps sprite_rg2_kernel at 86 VGPRs (5 waves per SIMD; 20 needed 146, 3 waves): SPRITE
-// 3.45 ms against 3.95 (200 kb x 1000, 20 000 clusters of <= 20 segments, profiles/r05_de)
-#define IGM_SPRITE_REG_BEADS 12
+// 20 needed 146 VGPRs (3 waves per SIMD): SPRITE 3.95 ms; 12 (86 VGPRs) 3.45 ms; 10 3.02 ms;
+// 8 (70 VGPRs) 3.07 ms (200 kb x 1000, 20 000 clusters of <= 20 segments, profiles/r05_de)
+#define IGM_SPRITE_REG_BEADS 10
 #endif
 constexpr int kRegBeads = IGM_SPRITE_REG_BEADS;
 template <class Bead>
