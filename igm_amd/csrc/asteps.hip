@@ -1016,13 +1016,24 @@ struct PolymerArgs {
 };
 
 __global__ void __launch_bounds__(kBT) polymer_kernel(PolymerArgs A) {
-    extern __shared__ float psm[];
+    extern __shared__ __attribute__((aligned(16))) float psm[];
     const int q = blockIdx.x;
     if (q >= A.nloci) return;
     const int S = A.S, nb = A.nbins, t = threadIdx.x;
     float* d = psm;
     int* cnt = reinterpret_cast<int*>(psm + S);  // nb counts, then the inclusive prefix
-    for (int b = t; b < nb; b += kBT) cnt[b] = 0;
+    // the bin tables staged in LDS (after the sort's scratch and the ranks): every structure's
+    // cdf search and rank lookup then costs LDS round trips instead of global ones
+    const int npad = pow2_at_least(S);
+    double* lcdf = reinterpret_cast<double*>(psm + ((S + nb + 2 * npad + S + 1) & ~1));
+    double* lvs = lcdf + nb;
+    int* lvp = reinterpret_cast<int*>(lvs + nb);
+    for (int b = t; b < nb; b += kBT) {
+        cnt[b] = 0;
+        lcdf[b] = A.cdf[b];
+        lvs[b] = A.vsort[b];
+        lvp[b] = A.vpos[b];
+    }
     __syncthreads();
     const int i = A.loci[q];
     const double* u = A.u + (size_t)q * S;
@@ -1035,10 +1046,10 @@ __global__ void __launch_bounds__(kBT) polymer_kernel(PolymerArgs A) {
         int lo = 0, hi = nb;  // first k with cdf[k] > u
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if (A.cdf[mid] <= uv) lo = mid + 1;
+            if (lcdf[mid] <= uv) lo = mid + 1;
             else hi = mid;
         }
-        atomicAdd(&cnt[A.vpos[lo < nb ? lo : nb - 1]], 1);
+        atomicAdd(&cnt[lvp[lo < nb ? lo : nb - 1]], 1);
     }
     __syncthreads();
     if (t < 64) {  // inclusive prefix over the bins: one wave, a chunk per lane
@@ -1058,7 +1069,6 @@ __global__ void __launch_bounds__(kBT) polymer_kernel(PolymerArgs A) {
     }
     __syncthreads();
     // the ranks of the distances (block_stable_rank)
-    const int npad = pow2_at_least(S);
     float* sk = reinterpret_cast<float*>(cnt + nb);
     int* si = reinterpret_cast<int*>(sk + npad);
     int* rk = si + npad;
@@ -1075,7 +1085,7 @@ __global__ void __launch_bounds__(kBT) polymer_kernel(PolymerArgs A) {
             if (cnt[mid] > r) hi = mid;
             else lo = mid + 1;
         }
-        A.out[row + s] = __double2float_rn(A.vsort[lo]);
+        A.out[row + s] = __double2float_rn(lvs[lo]);
         if (A.dist) A.dist[row + s] = ds;
     }
 }
@@ -1452,8 +1462,10 @@ extern "C" int igm_polymer_assign(igm_ctx* c, uint32_t flags, const float* xyz, 
     if (nbead < 2 || nstruct <= 0 || nloci < 0 || nbins <= 0 || !xyz || !edges || !prob ||
         (nloci > 0 && (!loci || !uniforms || !nn_dist)))
         return fail(c, IGM_E_INVALID, "igm_polymer_assign: invalid arguments");
-    const size_t lds = (size_t)nstruct * sizeof(float) + (size_t)nbins * sizeof(int) +
-                       (size_t)2 * pow2_at_least(nstruct) * sizeof(float) + (size_t)nstruct * sizeof(int);
+    // the distances, the bin counts, the sort's scratch, the ranks (8-byte aligned after), then
+    // the bin tables: cdf and values (double), value positions (int)
+    const size_t lds = (((size_t)nstruct + nbins + 2 * (size_t)pow2_at_least(nstruct) + nstruct + 1) & ~(size_t)1) *
+                           sizeof(float) + (size_t)nbins * (2 * sizeof(double) + sizeof(int));
     if (lds > (size_t)160 * 1024 - 1024)
         return fail(c, IGM_E_UNSUPPORTED, "igm_polymer_assign: %d structures x %d bins exceed the LDS-resident kernel",
                     nstruct, nbins);
