@@ -657,7 +657,11 @@ struct SpriteArgs {
 
 constexpr float kSpriteInf = 100000000.0f;  // INF of cpp_sprite_assignment.cpp:4
 constexpr int kMaxReps = 16;
-constexpr int kRegReps = 8;  // representatives whose copies a SPRITE thread keeps in registers
+// representatives whose copies a SPRITE thread keeps in registers: 6, the reference's default
+// max_chrom_in_cluster (SpriteAssignmentStep.py:114: clusters with more chromosomes are
+// skipped), so every computed cluster of a default configuration fits; 8 kept the kernel at 70
+// VGPRs against 61, SPRITE 2.98 / 3.00 ms against 2.81 / 2.83 (profiles/r05_de)
+constexpr int kRegReps = 6;
 
 // gyration_radius_sq (cpp_sprite_assignment.cpp:49-61): float mean accumulated in
 // order and divided by float(n), then the sum of X0*X0 + X1*X1 + X2*X2 in order / n
