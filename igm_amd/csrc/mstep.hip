@@ -4087,13 +4087,17 @@ int run_anneal(igm_ctx* c, const Prepared& pr, const igm_mstep_params* prm, floa
     // against the LDS engine's rule; 1.2/1.0/0.8 -3.0 %, 1.6/1.3/1.0 -2.7 %,
     // 1.8/1.5/1.2 +1.0 %; profiles/r04_ab/).
     const bool uniform_skin = prm->skin > 0 || getenv("IGM_SKIN_FACTOR") != nullptr;
+    float ra = 0.475f, rb = 0.25f, rhi = 1.4f;  // the population engine's rule (IGM_POP_SKIN_RULE "a,b,hi": tuning only)
+    if (const char* e = getenv("IGM_POP_SKIN_RULE")) {
+        if (sscanf(e, "%f,%f,%f", &ra, &rb, &rhi) != 3) return fail(c, IGM_E_INVALID, "IGM_POP_SKIN_RULE: a,b,hi");
+    }
     for (int k = 0; k < A.nseg; ++k) {
         if (uniform_skin) {
             A.seg_skin[k] = pr.P.skin;
         } else {
             const float rmax = 0.5f * (pr.P.cut_list - pr.P.skin);
             const float lt = log10f(fmaxf(A.seg_t0[k], 1.0f));
-            const float f = pr.big ? fminf(fmaxf(0.475f + 0.25f * lt, 0.4f), 1.4f)
+            const float f = pr.big ? fminf(fmaxf(ra + rb * lt, 0.4f), rhi)
                                    : fminf(fmaxf(0.45f + 0.15f * lt, 0.4f), 1.0f);
             A.seg_skin[k] = f * rmax;
         }
