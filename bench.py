@@ -78,11 +78,11 @@ def parse():
     return a
 
 
-def build_inputs(args, rank):
+def build_inputs(args, rank, first=None):
     from igm_amd import model as M
     from igm_amd import synthetic as syn
     from igm_amd._lib import pair_dtype
-    first = rank * args.nstruct
+    first = rank * args.nstruct if first is None else first
     pop = (syn.population_2mb if args.config == 'B' else syn.population_200kb)(args.nstruct, first_sid=first)
     atoms = M.Atoms(pop['radii'])
     natom = atoms.n
@@ -280,13 +280,13 @@ def bench_config_c(args, dev, world, rank, local, backend='nccl'):
     import torch
     import torch.distributed as dist
     from igm_amd.pipeline import AMIteration
+    from igm_amd.pipeline import shard
     total = args.c_total
-    if total % world:
-        raise ValueError('config C population %d does not split over %d ranks' % (total, world))
-    per = total // world
+    lo, hi = shard(total, rank, world)  # any population over any N (shards differ by at most one)
+    per = hi - lo
     ca = argparse.Namespace(**vars(args))
     ca.config, ca.nstruct, ca.sigma = 'C', per, 0.01  # protocol_scale: 1.0 for the metric
-    inp = build_inputs(ca, rank)
+    inp = build_inputs(ca, rank, first=lo)
     pop = inp['pop']
     it = AMIteration(dev, inp['xyz'], inp['atoms'], inp['chrom'], pop['copy_ptr'], pop['copy_idx'], inp['pairs'],
                      inp['prm'], inp['poly'], first_sid=inp['first'], rank=rank, world=world)

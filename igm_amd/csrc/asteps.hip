@@ -1094,6 +1094,134 @@ __global__ void __launch_bounds__(kBT) polymer_kernel(PolymerArgs A) {
     }
 }
 
+// ---- Populations past the LDS-resident rank kernels (fish_lds / polymer LDS > one CU's
+// LDS: about 4 000 / 8 000 structures).  The population size is unbounded in the reference
+// (ModelingStep.py:111, FishAssignmentStep.py:221-242, PolymerAssignmentStep.py:84-129), so
+// these take any S: the columns go to HBM scratch (kernel 1, one thread per (item,
+// structure)), and every structure's rank is counted against its whole column (kernel 2,
+// the column read in the same order by every lane: one broadcast load per step).  O(S^2)
+// compares per item, the same ranks as the sort (ties by structure index).
+__global__ void __launch_bounds__(kBT) fish_columns_kernel(FishArgs A, float* col) {
+    const int q = blockIdx.y, s = blockIdx.x * kBT + threadIdx.x;
+    if (q >= A.nitems || s >= A.S) return;
+    const int S = A.S;
+    int a0, na, b0 = 0, nb = 0;
+    if (A.kind == 0) {
+        const int h = A.items[q];
+        a0 = A.cptr[h];
+        na = A.cptr[h + 1] - a0;
+    } else {
+        const int h = A.items[2 * q], g = A.items[2 * q + 1];
+        a0 = A.cptr[h];
+        na = A.cptr[h + 1] - a0;
+        b0 = A.cptr[g];
+        nb = A.cptr[g + 1] - b0;
+    }
+    float mn = INFINITY, mx = -INFINITY;
+    for (int a = 0; a < na; ++a) {
+        float x, y, z;
+        load3(A.xyz, S, A.cidx[a0 + a], s, x, y, z);
+        if (A.kind == 0) {
+            const float d = norm3(x, y, z);
+            mn = d < mn ? d : mn;
+            mx = d > mx ? d : mx;
+        } else {
+            for (int b = 0; b < nb; ++b) {
+                float u, v, w;
+                load3(A.xyz, S, A.cidx[b0 + b], s, u, v, w);
+                const float d = norm3(__fsub_rn(x, u), __fsub_rn(y, v), __fsub_rn(z, w));
+                mn = d < mn ? d : mn;
+                mx = d > mx ? d : mx;
+            }
+        }
+    }
+    col[(size_t)q * 2 * S + s] = mn;
+    col[(size_t)q * 2 * S + S + s] = mx;
+}
+
+__global__ void __launch_bounds__(kBT) fish_count_kernel(FishArgs A, const float* col) {
+    const int q = blockIdx.y, s = blockIdx.x * kBT + threadIdx.x, S = A.S;
+    if (q >= A.nitems) return;
+    const float* vmin = col + (size_t)q * 2 * S;
+    const float* vmax = vmin + S;
+    const int ss = s < S ? s : S - 1;  // (lanes past S count along, store nothing)
+    const float mn = vmin[ss], mx = vmax[ss];
+    int rmin = 0, rmax = 0;
+    for (int t = 0; t < S; ++t) {
+        const float a = vmin[t], b = vmax[t];
+        rmin += (a < mn) | ((a == mn) & (t < ss));
+        rmax += (b < mx) | ((b == mx) & (t < ss));
+    }
+    if (s >= S) return;
+    const size_t row = (size_t)q * S;
+    if (A.omin) A.omin[row + s] = A.tmin[row + rmin];
+    if (A.omax) A.omax[row + s] = A.tmax[row + rmax];
+    if (A.dmin) A.dmin[row + s] = mn;
+    if (A.dmax) A.dmax[row + s] = mx;
+}
+
+// polymer past the LDS kernel: distances to HBM scratch and the per-locus bin histogram by
+// integer atomics (the same counts in any order), then ranks counted per structure and the
+// histogram's prefix (in the block's LDS, nb bins) searched as polymer_kernel does
+__global__ void __launch_bounds__(kBT) polymer_columns_kernel(PolymerArgs A, float* col, int* hist) {
+    const int q = blockIdx.y, s = blockIdx.x * kBT + threadIdx.x, S = A.S, nb = A.nbins;
+    if (q >= A.nloci || s >= S) return;
+    const int i = A.loci[q];
+    float x, y, z, a, b, c;
+    load3(A.xyz, S, i, s, x, y, z);
+    load3(A.xyz, S, i + 1, s, a, b, c);
+    col[(size_t)q * S + s] = norm3(__fsub_rn(x, a), __fsub_rn(y, b), __fsub_rn(z, c));
+    const double uv = A.u[(size_t)q * S + s];
+    int lo = 0, hi = nb;  // first k with cdf[k] > u
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (A.cdf[mid] <= uv) lo = mid + 1;
+        else hi = mid;
+    }
+    atomicAdd(&hist[(size_t)q * nb + A.vpos[lo < nb ? lo : nb - 1]], 1);
+}
+
+__global__ void __launch_bounds__(kBT) polymer_count_kernel(PolymerArgs A, const float* col, const int* hist) {
+    extern __shared__ int pcnt[];  // nb: the inclusive prefix of the locus' histogram
+    const int q = blockIdx.y, t = threadIdx.x, s = blockIdx.x * kBT + t, S = A.S, nb = A.nbins;
+    if (q >= A.nloci) return;
+    if (t < 64) {  // one wave, a chunk of bins per lane
+        const int* h = hist + (size_t)q * nb;
+        const int per = (nb + 63) / 64, b0 = t * per, b1 = min(nb, b0 + per);
+        int run = 0;
+        for (int b = b0; b < b1; ++b) run += h[b];
+        int incl = run;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (t >= o) incl += v;
+        }
+        run = incl - run;
+        for (int b = b0; b < b1; ++b) {
+            run += h[b];
+            pcnt[b] = run;
+        }
+    }
+    __syncthreads();
+    const float* d = col + (size_t)q * S;
+    const int ss = s < S ? s : S - 1;
+    const float ds = d[ss];
+    int r = 0;
+    for (int k = 0; k < S; ++k) {
+        const float e = d[k];
+        r += (e < ds) | ((e == ds) & (k < ss));
+    }
+    if (s >= S) return;
+    int lo = 0, hi = nb - 1;  // first value position whose prefix count exceeds r
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pcnt[mid] > r) hi = mid;
+        else lo = mid + 1;
+    }
+    const size_t row = (size_t)q * S;
+    A.out[row + s] = __double2float_rn(A.vsort[lo]);
+    if (A.dist) A.dist[row + s] = ds;
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -1243,8 +1371,9 @@ extern "C" int igm_fish_assign(igm_ctx* c, uint32_t flags, const float* xyz, int
         (kind != 0 && kind != 1) || (nitems > 0 && !items) || (out_min && !target_min) || (out_max && !target_max))
         return fail(c, IGM_E_INVALID, "igm_fish_assign: invalid arguments");
     const size_t lds = fish_lds(nstruct);
-    if (lds > (size_t)160 * 1024 - 1024)
-        return fail(c, IGM_E_UNSUPPORTED, "igm_fish_assign: %d structures exceed the LDS-resident rank kernel",
+    const bool big = lds > kSortLdsMax;  // past the LDS-resident rank kernel: columns in HBM, counted ranks
+    if (big && nitems > 65535)
+        return fail(c, IGM_E_UNSUPPORTED, "igm_fish_assign: %d items at %d structures exceed the grid", nitems,
                     nstruct);
     IGM_HIP_CHECK(c, hipSetDevice(c->device));
     if (nitems == 0) return IGM_OK;
@@ -1273,10 +1402,16 @@ extern "C" int igm_fish_assign(igm_ctx* c, uint32_t flags, const float* xyz, int
     IGM_TRY(out_device(c, flags, "fi_omax", out_max, nout, &d_omax));
     IGM_TRY(out_device(c, flags, "fi_dmin", dist_min, nout, &d_dmin));
     IGM_TRY(out_device(c, flags, "fi_dmax", dist_max, nout, &d_dmax));
-    if (lds > 65536) IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)fish_kernel,
-                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     FishArgs A{d_xyz, nstruct, d_cptr, d_cidx, kind, d_items, nitems, d_tmin, d_tmax, d_omin, d_omax, d_dmin, d_dmax};
-    {
+    if (big) {
+        void* col;
+        IGM_TRY(workspace(c, "fi_col", sizeof(float) * 2 * nout, &col));
+        Timed tm(c, "fish");
+        const dim3 g((unsigned)((nstruct + kBT - 1) / kBT), (unsigned)nitems);
+        hipLaunchKernelGGL(fish_columns_kernel, g, dim3(kBT), 0, c->stream, A, (float*)col);
+        hipLaunchKernelGGL(fish_count_kernel, g, dim3(kBT), 0, c->stream, A, (const float*)col);
+        IGM_HIP_CHECK(c, hipGetLastError());
+    } else {
         Timed tm(c, "fish");
         if (lds > 65536)
             IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)fish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1400,7 +1535,10 @@ extern "C" int igm_sprite_assign(igm_ctx* c, uint32_t flags, const float* xyz, i
             }
             for (int i = 0; i < ng; ++i) {
                 const int rg = seg_region[g0 + i];
-                ok = ok && ncopy(rg) <= 2;
+                // a segment takes its representative's copy bit: only when both have the same
+                // copies (a 2-copy segment under a 1-copy representative takes copy 0 in the
+                // index path, choice() = 0, but would read another representative's bit here)
+                ok = ok && ncopy(rg) <= 2 && (nr == 0 || ncopy(rg) == ncopy(rep_region[r0 + seg_rep[g0 + i]]));
                 sb2[g0 + i] = b2(rg);
                 sbit[g0 + i] = nr > 0 ? rbit[r0 + seg_rep[g0 + i]] : 0;
             }
@@ -1470,9 +1608,12 @@ extern "C" int igm_polymer_assign(igm_ctx* c, uint32_t flags, const float* xyz, 
     // the bin tables: cdf and values (double), value positions (int)
     const size_t lds = (((size_t)nstruct + nbins + 2 * (size_t)pow2_at_least(nstruct) + nstruct + 1) & ~(size_t)1) *
                            sizeof(float) + (size_t)nbins * (2 * sizeof(double) + sizeof(int));
-    if (lds > (size_t)160 * 1024 - 1024)
-        return fail(c, IGM_E_UNSUPPORTED, "igm_polymer_assign: %d structures x %d bins exceed the LDS-resident kernel",
-                    nstruct, nbins);
+    // past the LDS-resident kernel: distances and histograms in HBM, counted ranks (the
+    // prefix of one locus' histogram in LDS)
+    const bool big = lds > kSortLdsMax;
+    if (big && ((size_t)nbins * sizeof(int) > kSortLdsMax || nloci > 65535))
+        return fail(c, IGM_E_UNSUPPORTED, "igm_polymer_assign: %d loci x %d bins at %d structures exceed the kernels",
+                    nloci, nbins, nstruct);
     IGM_HIP_CHECK(c, hipSetDevice(c->device));
     if (nloci == 0) return IGM_OK;
     if (flags & IGM_DEVICE_PTRS)
@@ -1508,11 +1649,26 @@ extern "C" int igm_polymer_assign(igm_ctx* c, uint32_t flags, const float* xyz, 
     float *d_out, *d_dist;
     IGM_TRY(out_device(c, flags, "po_out", nn_dist, nout, &d_out));
     IGM_TRY(out_device(c, flags, "po_dist", dist, nout, &d_dist));
-    if (lds > 65536)
-        IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)polymer_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds));
     PolymerArgs A{d_xyz, nstruct, d_loci, nloci, d_u, nbins, d_cdf, d_vpos, d_vsort, d_out, d_dist};
-    {
+    if (big) {
+        void *col, *hist;
+        IGM_TRY(workspace(c, "po_col", sizeof(float) * nout, &col));
+        IGM_TRY(workspace(c, "po_hist", sizeof(int) * (size_t)nloci * nbins, &hist));
+        IGM_HIP_CHECK(c, hipMemsetAsync(hist, 0, sizeof(int) * (size_t)nloci * nbins, c->stream));
+        const size_t hl = sizeof(int) * (size_t)nbins;
+        if (hl > 65536)
+            IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)polymer_count_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl));
+        Timed tm(c, "polymer");
+        const dim3 g((unsigned)((nstruct + kBT - 1) / kBT), (unsigned)nloci);
+        hipLaunchKernelGGL(polymer_columns_kernel, g, dim3(kBT), 0, c->stream, A, (float*)col, (int*)hist);
+        hipLaunchKernelGGL(polymer_count_kernel, g, dim3(kBT), hl, c->stream, A, (const float*)col,
+                           (const int*)hist);
+        IGM_HIP_CHECK(c, hipGetLastError());
+    } else {
+        if (lds > 65536)
+            IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)polymer_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         Timed tm(c, "polymer");
         hipLaunchKernelGGL(polymer_kernel, dim3((unsigned)nloci), dim3(kBT), lds, c->stream, A);
         IGM_HIP_CHECK(c, hipGetLastError());

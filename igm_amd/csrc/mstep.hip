@@ -1324,6 +1324,7 @@ constexpr int kPopMaxGroups = 64;  // structure groups (streams) of one run: bui
 // effect at protocol x0.1, had measured 49 152 0.8 % faster than 32 768.)
 constexpr int kPopCellCap = IGM_POP_CELL_CAP;
 constexpr int kPopCells = kPopCellCap + 2;  // cell offsets of a structure: real cells, non-bead run, end
+constexpr int kPopCntStride = (kPopCells + 3) & ~3;  // cell counts of a structure (16-byte rows)
 #ifndef IGM_POP_FILL_W
 #define IGM_POP_FILL_W 2
 #endif
@@ -1487,6 +1488,10 @@ struct PopArgs {
     int* flist2;         // (B) the structures whose inner list is rebuilt this step
     int* nflag2;         // (1)
     unsigned long long* sprof;  // optional (8): the sort kernel's phase cycles, summed (profiling)
+    // The split sort (pop_grid .. pop_rank, several 256-thread workgroups per flagged
+    // structure instead of one 1024-thread workgroup holding the grid in LDS):
+    int* ccnt;           // (B, kPopCntStride) cell counts; zero between builds (the scan clears them)
+    int* tid;            // (B, ldn) atom ids scattered into their cells (before the in-cell rank)
 };
 
 // one Verlet list of the engine (the inner one, or the outer one of two-level lists)
@@ -1668,6 +1673,45 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
     }
 }
 
+// The cell grid of build_nlist for structure s from its bead bounding box mm = {max -x,
+// -y, -z, max x, y, z}: cells of side cs >= cut_list in y and z, cs / qx in x (the sort
+// order is x-fastest, so an x run of cells stays one slot range, and a slot's list build
+// visits only the x cells its cut_list sphere meets in each row), at most A.ccap cells.
+// Stored to gp (lo[3], inv[3]) and gn (nb[3], x reach); sg/sn get lo, inv and nb.
+__device__ __forceinline__ void pop_grid_of(const PopArgs& A, int s, const float (&mm)[6], float* sg, int* sn) {
+    float ext[3], vol = 1.0f;
+    const float cut = A.P.cut_list;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        ext[d] = mm[3 + d] + mm[d];
+        if (!(ext[d] >= 0.0f)) ext[d] = 0.0f;
+        vol *= fmaxf(ext[d], cut);
+    }
+    float cs = cut;
+    const float cap = (float)A.ccap, qx = (float)A.qx;
+    if (vol * qx / (cs * cs * cs) > cap) cs = cbrtf(vol * qx / cap) * 1.0001f;
+    float* gp = A.gp + (size_t)s * 8;
+    int* gn = A.gn + (size_t)s * 8;
+    int nbv[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        nbv[d] = (int)floorf(d == 0 ? ext[d] * qx / cs : ext[d] / cs);
+        if (nbv[d] < 1) nbv[d] = 1;
+    }
+    // x cells a pair within cut_list can be apart (the cell walk's x reach)
+    gn[3] = ext[0] > 0.0f ? max(1, (int)ceilf(cut * (float)nbv[0] / ext[0] * 1.00001f)) : 1;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const int nbd = nbv[d];
+        sg[d] = -mm[d];
+        sg[3 + d] = ext[d] > 0.0f ? (float)nbd / ext[d] : 0.0f;
+        sn[d] = nbd;
+        gp[d] = sg[d];
+        gp[3 + d] = sg[3 + d];
+        gn[d] = nbd;
+    }
+}
+
 // One workgroup per flagged structure: the cell grid of build_nlist (cells of side >=
 // cut_list, at most kPopCellCap) from the bbox partials, then a counting sort of the
 // slots into it -- cell counts as packed u16 pairs in LDS, and with IDS_LDS the new
@@ -1727,40 +1771,7 @@ __global__ void __launch_bounds__(kPopSortNT) pop_sort_kernel(PopArgs A, int fp)
         float mm[6];
 #pragma unroll
         for (int d = 0; d < 6; ++d) mm[d] = smm[d];
-        float ext[3], vol = 1.0f;
-        const float cut = A.P.cut_list;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            ext[d] = mm[3 + d] + mm[d];
-            if (!(ext[d] >= 0.0f)) ext[d] = 0.0f;
-            vol *= fmaxf(ext[d], cut);
-        }
-        // cells of side cs >= cut_list in y and z, cs / qx in x (the sort order is
-        // x-fastest, so an x run of cells stays one slot range, and a slot's list build
-        // visits only the x cells its cut_list sphere meets in each row)
-        float cs = cut;
-        const float cap = (float)A.ccap, qx = (float)A.qx;
-        if (vol * qx / (cs * cs * cs) > cap) cs = cbrtf(vol * qx / cap) * 1.0001f;
-        float* gp = A.gp + (size_t)s * 8;
-        int* gn = A.gn + (size_t)s * 8;
-        int nbv[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            nbv[d] = (int)floorf(d == 0 ? ext[d] * qx / cs : ext[d] / cs);
-            if (nbv[d] < 1) nbv[d] = 1;
-        }
-        // x cells a pair within cut_list can be apart (the cell walk's x reach)
-        gn[3] = ext[0] > 0.0f ? max(1, (int)ceilf(cut * (float)nbv[0] / ext[0] * 1.00001f)) : 1;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const int nbd = nbv[d];
-            sg[d] = -mm[d];
-            sg[3 + d] = ext[d] > 0.0f ? (float)nbd / ext[d] : 0.0f;
-            sn[d] = nbd;
-            gp[d] = sg[d];
-            gp[3 + d] = sg[3 + d];
-            gn[d] = nbd;
-        }
+        pop_grid_of(A, s, mm, sg, sn);
     }
     __syncthreads();
     const float lo[3] = {sg[0], sg[1], sg[2]}, inv[3] = {sg[3], sg[4], sg[5]};
@@ -1944,22 +1955,163 @@ inline int pop_sort_cells(int natom) {
 }
 static_assert(kPopCells < 65536, "cell ids are packed in 16 bits");
 
-// logical block of the build kernels over the compacted flagged structures (plain
-// order: the working blocks are dealt over all XCDs); false for an idle block
-__device__ __forceinline__ bool pop_build_slot(const PopArgs& A, int* s, int* i) {
-    const int k = blockIdx.x / A.nbs;
-    if (k >= *A.nflag) return false;
-    *s = A.flist[k];
-    *i = (blockIdx.x % A.nbs) * kPopBS + threadIdx.x;
-    return *i < A.cm.natom;
+// ---- The split sort: the same slot order as pop_sort_kernel (same grid, same cells, ids
+// ascending inside a cell), built by several 256-thread workgroups per flagged structure
+// over the compacted list of flagged structures, with the counts and ids in HBM/L2 instead
+// of one CU's LDS.  pop_sort_kernel holds 124 KB of LDS for ~200 us per flagged structure
+// (one workgroup's chain of dependent LDS round trips); at 125 structures per GPU ~10 such
+// workgroups sit on every step's critical path, and at pop = 1000 their LDS keeps the other
+// structure group's kernels off the CUs they occupy (profiles/r05_ab).
+//   pop_grid     one wave per structure: flagged ones get their grid and a flist entry
+//   pop_count    per slot: its cell, and its arrival rank there (global atomic), key = c << 16 | rank
+//   pop_scan     per flagged structure: cell offsets (exclusive scan), counts cleared, parity flipped
+//   pop_scatter  per slot: its atom id at its cell's first slot + arrival rank
+//   pop_rank     per slot: new slot = cell's first slot + ids of the cell below its own
+// The arrival ranks differ run to run; the in-cell order (ascending ids) does not.
+// Build kernels over the flagged structures run a grid of `per` structure slots x nbs
+// blocks, and block b takes flagged structures b / nbs, + per, ... (*nflag of them).
+__global__ void __launch_bounds__(256) pop_grid_kernel(PopArgs A, int fp) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, s = blockIdx.x * 4 + w;
+    if (s >= A.cm.nstruct || !A.flag[fp][s]) return;  // (wave-uniform)
+    const float* bp = A.bbp + (size_t)s * A.nbs * 6;
+    float mm[6];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) mm[d] = -3.0e38f;
+    for (int b = lane; b < A.nbs; b += 64)
+#pragma unroll
+        for (int d = 0; d < 6; ++d) mm[d] = fmaxf(mm[d], bp[b * 6 + d]);
+#pragma unroll
+    for (int d = 0; d < 6; ++d) mm[d] = wave_max_f32(mm[d]);
+    if (lane == 0) {
+        A.flist[atomicAdd(A.nflag, 1)] = s;
+        float sg[6];
+        int sn[3];
+        pop_grid_of(A, s, mm, sg, sn);
+    }
+}
+
+__global__ void __launch_bounds__(kPopBS) pop_count_kernel(PopArgs A) {
+    const int nf = *A.nflag, per = gridDim.x / A.nbs, i = (blockIdx.x % A.nbs) * kPopBS + threadIdx.x;
+    if (i >= A.cm.natom) return;
+    for (int k = blockIdx.x / A.nbs; k < nf; k += per) {
+        const int s = A.flist[k];
+        const size_t base = (size_t)s * A.cm.ldn;
+        const float* gp = A.gp + (size_t)s * 8;
+        const int* gn = A.gn + (size_t)s * 8;
+        const float lo[3] = {gp[0], gp[1], gp[2]}, inv[3] = {gp[3], gp[4], gp[5]};
+        const int nb[3] = {gn[0], gn[1], gn[2]};
+        const float4 p = A.buf[A.par[s]].pos[base + i];
+        const int c = p.w >= 0.0f ? pop_cell_index(p.x, p.y, p.z, lo, inv, nb) : pop_ncell(nb);
+        const int r = atomicAdd(A.ccnt + (size_t)s * kPopCntStride + c, 1);
+        A.remap[base + i] = (c << 16) | r;
+    }
+}
+
+// exclusive scan of the counts of cells 0..ncell (the last one the non-bead run) into the
+// cell offsets (cell[ncell + 1] = N), 8 cells per thread and tile; counts cleared behind
+template <int NT>
+__global__ void __launch_bounds__(NT) pop_scan_kernel(PopArgs A) {
+    __shared__ int wsum[NT / 64];
+    const int nf = *A.nflag, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int k = blockIdx.x; k < nf; k += gridDim.x) {
+        const int s = A.flist[k];
+        const int* gn = A.gn + (size_t)s * 8;
+        const int n = gn[0] * gn[1] * gn[2] + 1;  // cells and the non-bead run
+        int4* cnt = reinterpret_cast<int4*>(A.ccnt + (size_t)s * kPopCntStride);
+        int* cg = A.cell + (size_t)s * kPopCells;
+        int run = 0;  // offsets of the tiles before (block-uniform)
+        for (int c0 = 0; c0 < n; c0 += 8 * NT) {
+            const int c = c0 + 8 * t;
+            int4 a = make_int4(0, 0, 0, 0), b = make_int4(0, 0, 0, 0);
+            if (c < n) {  // (the stride rounds the rows to 4: c + 4 < kPopCntStride)
+                a = cnt[c >> 2];
+                b = c + 4 < n ? cnt[(c >> 2) + 1] : make_int4(0, 0, 0, 0);
+            }
+            const int v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            int sum = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sum += v[u];
+            int incl = sum;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(incl, off);
+                if (lane >= off) incl += y;
+            }
+            if (lane == 63) wsum[w] = incl;
+            __syncthreads();
+            int ex = run + incl - sum, tile = 0;
+            for (int q = 0; q < NT / 64; ++q) {
+                ex += q < w ? wsum[q] : 0;
+                tile += wsum[q];
+            }
+            if (c < n) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    if (c + u < n) cg[c + u] = ex;
+                    ex += v[u];
+                }
+                const int4 z = make_int4(0, 0, 0, 0);
+                cnt[c >> 2] = z;
+                if (c + 4 < n) cnt[(c >> 2) + 1] = z;
+            }
+            run += tile;
+            __syncthreads();  // (wsum reused by the next tile)
+        }
+        if (t == 0) {
+            cg[n] = run;  // = N
+            A.par[s] ^= 1;  // the slot order being built is the other buffer's
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kPopBS) pop_scatter_kernel(PopArgs A) {
+    const int nf = *A.nflag, per = gridDim.x / A.nbs, i = (blockIdx.x % A.nbs) * kPopBS + threadIdx.x;
+    if (i >= A.cm.natom) return;
+    for (int k = blockIdx.x / A.nbs; k < nf; k += per) {
+        const int s = A.flist[k];
+        const size_t base = (size_t)s * A.cm.ldn;
+        const uint32_t key = (uint32_t)A.remap[base + i];
+        const int* cg = A.cell + (size_t)s * kPopCells;
+        A.tid[base + cg[key >> 16] + (key & 0xffffu)] = A.buf[A.par[s] ^ 1].aid[base + i];
+    }
+}
+
+__global__ void __launch_bounds__(kPopBS) pop_rank_kernel(PopArgs A) {
+    const int nf = *A.nflag, per = gridDim.x / A.nbs, i = (blockIdx.x % A.nbs) * kPopBS + threadIdx.x;
+    if (i >= A.cm.natom) return;
+    for (int k = blockIdx.x / A.nbs; k < nf; k += per) {
+        const int s = A.flist[k];
+        const size_t base = (size_t)s * A.cm.ldn;
+        const uint32_t key = (uint32_t)A.remap[base + i];
+        const int c = (int)(key >> 16);
+        const int* cg = A.cell + (size_t)s * kPopCells;
+        const int beg = cg[c], end = cg[c + 1];
+        const int q = A.par[s], a = A.buf[q ^ 1].aid[base + i];
+        const int* id = A.tid + base;
+        int r = 0;
+        for (int j = beg; j < end; ++j) r += id[j] < a ? 1 : 0;
+        const int n = beg + r;
+        A.buf[q].aid[base + n] = a;
+        A.buf[q].slot[base + a] = n;
+        A.remap[base + i] = n;  // (old slot i -> new slot)
+        A.inv[base + n] = i;
+    }
 }
 
 // state (and with BONDS the bonds; the fused force kernel re-indexes them itself) of
-// every slot of a flagged structure into its new slot order
+// every slot of a flagged structure into its new slot order.  Over the compacted flagged
+// structures: block b takes structures b / nbs, + per, ... (plain order: the working
+// blocks are dealt over all XCDs)
+template <bool BONDS>
+__device__ __forceinline__ void pop_permute_slot(const PopArgs& A, int s, int i);
 template <bool BONDS>
 __global__ void __launch_bounds__(kPopBS) pop_permute_kernel(PopArgs A) {
-    int s, i;
-    if (!pop_build_slot(A, &s, &i)) return;
+    const int nf = *A.nflag, per = gridDim.x / A.nbs, i = (blockIdx.x % A.nbs) * kPopBS + threadIdx.x;
+    if (i >= A.cm.natom) return;
+    for (int k = blockIdx.x / A.nbs; k < nf; k += per) pop_permute_slot<BONDS>(A, A.flist[k], i);
+}
+template <bool BONDS>
+__device__ __forceinline__ void pop_permute_slot(const PopArgs& A, int s, int i) {
     const size_t base = (size_t)s * A.cm.ldn, k = base + i;
     const int q = A.par[s], p = q ^ 1;
     const PopBuf &O = A.buf[p], &B = A.buf[q];
@@ -2119,18 +2271,19 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
 template <int ROW>
 __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
     __shared__ uint32_t lrow[kPopBS * ROW / 2];
-    const int kb = blockIdx.x / A.nbs;
-    if (kb >= *A.nflag) return;  // an idle block (the structure was not flagged)
-    const int s = A.flist[kb], blk = blockIdx.x % A.nbs, t = threadIdx.x, i = blk * kPopBS + t;
+    const int nf = *A.nflag, per = gridDim.x / A.nbs, t = threadIdx.x, i = (blockIdx.x % A.nbs) * kPopBS + t;
     if (i >= A.cm.natom) return;
-    const size_t base = (size_t)s * A.cm.ldn;
-    const float4* pos = A.buf[A.par[s]].pos + base;
-    const float4 p0 = pos[i];
-    const PopList T = A.two ? PopList{A.nlo, A.nnbo, A.kqo} : PopList{A.nl, A.nnb, A.kq};
-    if (p0.w >= 0.0f)
-        pop_fill_slot<true>(A, T, s, i, base, pos, p0, lrow + t * (ROW / 2), ROW - 2);
-    else
-        T.nnb[base + i] = 0;
+    for (int kb = blockIdx.x / A.nbs; kb < nf; kb += per) {  // (idle blocks: no flagged structure left)
+        const int s = A.flist[kb];
+        const size_t base = (size_t)s * A.cm.ldn;
+        const float4* pos = A.buf[A.par[s]].pos + base;
+        const float4 p0 = pos[i];
+        const PopList T = A.two ? PopList{A.nlo, A.nnbo, A.kqo} : PopList{A.nl, A.nnb, A.kq};
+        if (p0.w >= 0.0f)
+            pop_fill_slot<true>(A, T, s, i, base, pos, p0, lrow + t * (ROW / 2), ROW - 2);
+        else
+            T.nnb[base + i] = 0;
+    }
 }
 
 // Two-level lists: the inner Verlet list (cut_in) of every slot of a structure whose
@@ -3622,6 +3775,10 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     }
     V.inv = Q.inv + o;
     V.remap = Q.remap + o;
+    if (Q.ccnt) {
+        V.ccnt = Q.ccnt + (size_t)s0 * kPopCntStride;
+        V.tid = Q.tid + o;
+    }
     V.flag[0] = Q.flag[0] + s0;
     V.flag[1] = Q.flag[1] + s0;
     V.oflag[0] = Q.oflag[0] + s0;
@@ -3672,8 +3829,8 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         // 2 x 2, slot remaps 8; per structure the cell offsets.  At config C (1000 x 29 839
         // slots) the lists alone are 15.3 GB.  Checked against the free HBM (plus what this
         // context's population workspace already holds) before anything is allocated.
-        const size_t per_slot = 2 * (16 + 12 + 12 + 4 + 4 + 1) + 12 + 8 * (size_t)Q.kq + 2 + 8 * (size_t)Q.bdmax + 4 + 8;
-        const size_t need = per_slot * SL + sizeof(int) * (size_t)S * kPopCells;
+        const size_t per_slot = 2 * (16 + 12 + 12 + 4 + 4 + 1) + 12 + 8 * (size_t)Q.kq + 2 + 8 * (size_t)Q.bdmax + 4 + 8 + 4;
+        const size_t need = per_slot * SL + sizeof(int) * (size_t)S * (kPopCells + kPopCntStride);
         size_t held = 0;
         for (const auto& kv : c->ws)
             if (kv.first.compare(0, 4, "pop_") == 0) held += kv.second.second;
@@ -3836,15 +3993,30 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                      : N <= 32 * kPopSortNT ? pop_sort_kernel<true, 32> : pop_sort_kernel<true, 0>;
     IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)sort_kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)sort_lds));
+    auto knob = [](const char* name, int dflt) {
+        const char* e = getenv(name);
+        return e ? atoi(e) : dflt;
+    };
+    // the split sort (default; IGM_POP_SORT=0: the single-workgroup LDS sort, A/B only --
+    // both give the same slot order); two-level lists and the fused engine keep the LDS sort
+    const bool split = knob("IGM_POP_SORT", 1) != 0 && !Q.two && !kPopFused;
+    if (split) {
+        void *pcc, *ptd;
+        IGM_TRY(workspace(c, "pop_ccnt", sizeof(int) * (size_t)S * kPopCntStride, &pcc));
+        IGM_TRY(workspace(c, "pop_tid", sizeof(int) * SL, &ptd));
+        IGM_HIP_CHECK(c, hipMemsetAsync(pcc, 0, sizeof(int) * (size_t)S * kPopCntStride, c->stream));
+        Q.ccnt = (int*)pcc;
+        Q.tid = (int*)ptd;
+    }
+    // structure slots of the build kernels' grids (IGM_POP_BUILD_SLOTS): a block loops over
+    // the flagged structures b / nbs, + slots, ..., so the grid need not cover every
+    // structure of the group (~1/6 of them rebuild at a step)
+    const int bslots = std::max(1, knob("IGM_POP_BUILD_SLOTS", 128));
     // Structure groups on auxiliary streams: while one group waits in its latency-bound
     // sort, the others' force and integrate launches fill the CUs (measured on config C:
     // 2 groups 11 % faster than 1, 4 and 8 slower).  Tuning knobs: IGM_POP_GROUPS groups,
     // IGM_POP_CONC of them in flight together, IGM_POP_CHUNK steps per group before the
     // next ones run (0: every group advances in lock step).
-    auto knob = [](const char* name, int dflt) {
-        const char* e = getenv(name);
-        return e ? atoi(e) : dflt;
-    };
     int ng = knob("IGM_POP_GROUPS", 2), nc = knob("IGM_POP_CONC", 0), chunk = knob("IGM_POP_CHUNK", 0);
     ng = ng < 1 ? 1 : (ng > S ? S : (ng > kPopMaxGroups ? kPopMaxGroups : ng));
     nc = nc < 1 || nc > ng ? ng : nc;
@@ -3937,14 +4109,24 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                     for (int g = w0; g < w0 + nc && g < ng; ++g) {
                         const int ns = g0[g + 1] - g0[g];
                         hipStream_t sg = strm(g);
+                        const dim3 bgrid(std::min(ns, bslots) * Q.nbs);  // the build kernels' grid
                         hipLaunchKernelGGL(pop_integrate_kernel, grid_of(g), blk, 0, sg, V[g], st);
-                        hipLaunchKernelGGL(sort_kern, dim3(ns), dim3(kPopSortNT), sort_lds, sg, V[g], st.fp);
-                        hipLaunchKernelGGL(pop_permute_kernel<!kPopFused>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                        if (split) {
+                            hipLaunchKernelGGL(pop_grid_kernel, dim3((ns + 3) / 4), dim3(256), 0, sg, V[g], st.fp);
+                            hipLaunchKernelGGL(pop_count_kernel, bgrid, blk, 0, sg, V[g]);
+                            hipLaunchKernelGGL(pop_scan_kernel<1024>, dim3(std::min(ns, bslots)), dim3(1024), 0, sg,
+                                               V[g]);
+                            hipLaunchKernelGGL(pop_scatter_kernel, bgrid, blk, 0, sg, V[g]);
+                            hipLaunchKernelGGL(pop_rank_kernel, bgrid, blk, 0, sg, V[g]);
+                        } else {
+                            hipLaunchKernelGGL(sort_kern, dim3(ns), dim3(kPopSortNT), sort_lds, sg, V[g], st.fp);
+                        }
+                        hipLaunchKernelGGL(pop_permute_kernel<!kPopFused>, bgrid, blk, 0, sg, V[g]);
                         if (Q.two) {
-                            hipLaunchKernelGGL(pop_fill_kernel<kOuterRow>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                            hipLaunchKernelGGL(pop_fill_kernel<kOuterRow>, bgrid, blk, 0, sg, V[g]);
                             hipLaunchKernelGGL(pop_refilter_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
                         } else if (!kPopFused) {
-                            hipLaunchKernelGGL(pop_fill_kernel<kPopListRow>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                            hipLaunchKernelGGL(pop_fill_kernel<kPopListRow>, bgrid, blk, 0, sg, V[g]);
                         }
                         hipLaunchKernelGGL(pop_force_kernel<kPopFused>, grid_of(g), blk, 0, sg, V[g], evf, envf, st);
                         if (pst && step % stats_every == 0)

@@ -71,17 +71,28 @@ def _staged(t, group):
     return t.is_cuda and dist.get_backend(group) == 'gloo'
 
 
-def gather_population(xyz_local, group=None):
+def gather_population(xyz_local, group=None, counts=None):
     """Every rank's (S_local, natom, 3) block -> the (S_total, natom, 3) population
-    in rank order (one all-gather; RCCL over xGMI on the GPUs)."""
+    in rank order (one all-gather; RCCL over xGMI on the GPUs).  counts: the structures
+    of every rank (pipeline.shard of any population size -- ModelingStep.py:111 runs
+    range(population_size), any size); unequal blocks travel padded to the largest
+    and are cut back to their counts."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     host = _staged(xyz_local, group)
     src = xyz_local.contiguous().cpu() if host else xyz_local.contiguous()
+    n = src.shape[0]
+    if counts is None:
+        counts = [n] * world
+    if counts.count(counts[0]) != len(counts):  # uneven shards: pad to the largest block
+        big = max(counts)
+        pad = src.new_zeros((big,) + tuple(src.shape[1:]))
+        pad[:n] = src
+        src = pad
     parts = [torch.empty_like(src) for _ in range(world)]
     dist.all_gather(parts, src, group=group)
-    out = torch.cat(parts, 0)
+    out = torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
     return out.to(xyz_local.device) if host else out
 
 
@@ -142,12 +153,11 @@ class AMIteration(object):
         xyz_local = np.ascontiguousarray(xyz_local, np.float32)
         self.S_local, self.natom = xyz_local.shape[0], xyz_local.shape[1]
         self.nbead = int(atoms.nbead)
-        if self.coll:  # gather_population all-gathers equal blocks: every rank must hold as many structures
-            counts = self._all_counts(self.S_local)
-            if len(set(counts)) != 1:
-                raise ValueError('structure shards must be equal (got %s per rank): pad the population to a '
-                                 'multiple of the world size' % counts)
-        self.S_total = self.S_local * world
+        # every rank's structure count (shards of any population size may differ by one;
+        # gather_population pads them), this rank's first column in the population
+        self.counts = self._all_counts(self.S_local) if self.coll else [self.S_local] * world
+        self.s_off = sum(self.counts[:rank])
+        self.S_total = sum(self.counts)
         self.xyz = T(xyz_local)                                  # (S_local, natom, 3) M-step layout
         self.radii = T(atoms.radii)
         self.flags = T(atoms.flags)
@@ -206,7 +216,7 @@ class AMIteration(object):
         torch = self.torch
         P = _lib.ptr
         if self.coll:
-            src = gather_population(self.xyz, self.group)
+            src = gather_population(self.xyz, self.group, self.counts)
         else:
             src = self.xyz
         # (S_total, natom, 3) -> (nbead, S_total, 3): the .hss / A-step layout
@@ -293,7 +303,7 @@ class AMIteration(object):
         it_corr state of ActivationDistanceStep), the non-bead atoms' coordinates."""
         from . import hss
         P = _lib.ptr
-        src = gather_population(self.xyz, self.group) if self.coll else self.xyz
+        src = gather_population(self.xyz, self.group, self.counts) if self.coll else self.xyz
         self._call('igm_population_transpose', IGM_DEVICE_PTRS, self.nbead, self.S_total, self.natom, P(src),
                    P(self.pop_bm), 1)
         pairs_u8 = self.pairs[:self.npairs * pair_dtype.itemsize]
@@ -340,8 +350,8 @@ class AMIteration(object):
         if len(pi) != self.npairs_total:
             raise ValueError('checkpoint %s holds a different pair list' % path)
         # checkpoint() wrote the ranks' blocks in rank order: this rank's structures are
-        # columns rank*S_local .. (whatever its first structure id is)
-        s0 = self.rank * self.S_local
+        # columns s_off .. s_off + S_local (whatever its first structure id is)
+        s0 = self.s_off
         x = np.zeros((self.S_local, self.natom, 3), np.float32)
         x[:, :self.nbead] = crd[:, s0:s0 + self.S_local].transpose(1, 0, 2)
         x[:, self.nbead:] = extra[s0:s0 + self.S_local]

@@ -15,38 +15,9 @@ satisfied), where the final state does not depend on K at all.  `random_contacts
 adds Hi-C-like restraints that cannot all be met, so the final energies balance the
 bond, soft-pair and envelope terms and respond to each of them.
 """
-import json
-
 import numpy as np
 
-
-def scaled_protocol(protocol, scale):
-    """The protocol with every MD step count scaled (all stages, relax and CG kept)."""
-    p = json.loads(json.dumps(protocol))
-    cap = p['custom_annealing_protocol']
-    cap['mdsteps'] = [max(1, int(round(n * scale))) for n in cap['mdsteps']]
-    cap['relax']['mdsteps'] = max(1, int(round(cap['relax']['mdsteps'] * scale)))
-    return p
-
-
-def random_contacts(radii, nbead, nlocal, nlong, seed, cr=2.0, k=1.0):
-    """Hi-C-like bonds (harmonic upper bound, r0 = cr (r_i + r_j)): nlocal pairs at
-    genomic separations 2..60 beads, nlong between random beads."""
-    from igm_amd import model as M
-    from igm_amd._lib import bond_dtype
-    rng = np.random.default_rng(seed)
-    i1 = rng.integers(0, nbead - 61, nlocal)
-    j1 = i1 + rng.integers(2, 61, nlocal)
-    i2 = rng.integers(0, nbead, nlong)
-    j2 = rng.integers(0, nbead, nlong)
-    i = np.concatenate([i1, i2])
-    j = np.concatenate([j1, j2])
-    keep = i != j
-    b = np.zeros(int(keep.sum()), bond_dtype)
-    b['i'], b['j'] = i[keep], j[keep]
-    b['r0'] = M.r0_contact(cr, radii[b['i']], radii[b['j']]).astype(np.float32)
-    b['k'] = k
-    return b
+from igm_amd.workloads import random_contacts, scaled_protocol  # noqa: E402,F401  (shared with the bench)
 
 
 def violation_fraction(x, bonds, tol=0.05):

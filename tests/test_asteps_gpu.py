@@ -186,10 +186,11 @@ def test_fish_task_dict_and_ties(pop):
     assert np.array_equal(omin[0], t[0])
 
 
-@pytest.mark.parametrize('S', [50, 200, 256, 300, 512, 700, 1024, 1500, 2048, 2100])
+@pytest.mark.parametrize('S', [50, 200, 256, 300, 512, 700, 1024, 1500, 2048, 2100, 4096, 5000, 10000])
 def test_fish_rank_widths_with_ties(S):
     """The rank sort at every width it takes (registers for npad = 256, 512, 1024, 2048;
-    LDS otherwise): radial distances rounded to a few values, so most ranks are decided by
+    LDS otherwise; past one CU's LDS, S = 5000 and 10000, the columns in HBM and counted
+    ranks): radial distances rounded to a few values, so most ranks are decided by
     structure order, against the oracle's argsort(argsort(kind='stable'))."""
     from igm_amd import fish
     rng = np.random.default_rng(S)
@@ -266,6 +267,26 @@ def test_sprite_table_path_equals_index_path(pop, monkeypatch):
     for mode in ('1', '0'):
         monkeypatch.setenv('IGM_SPRITE_TABLES', mode)
         out.append(sprite.rg2_select(pop['coordinates'], pop['copy_ptr'], pop['copy_idx'], t, 5, return_rg2=True))
+    for a, b in zip(*out):
+        assert np.array_equal(bits(a) if a.dtype == np.float32 else a, bits(b) if b.dtype == np.float32 else b)
+
+
+def test_sprite_table_path_mixed_copies(monkeypatch):
+    """A 2-copy segment under a 1-copy representative (and a 2-copy one under a 2-copy
+    representative): the table path must pick the copies the index path picks."""
+    from igm_amd import sprite
+    rng = np.random.default_rng(3)
+    S = 300
+    xyz = rng.normal(0.0, 1.0, (7, S, 3)).astype(np.float32)
+    copy_ptr = np.array([0, 1, 3, 5, 7], np.int32)  # region 0: 1 copy, regions 1-3: 2 copies
+    copy_idx = np.arange(7, dtype=np.int32)
+    i32 = lambda a: np.asarray(a, np.int32)
+    t = dict(seg_ptr=i32([0, 3, 5]), seg_region=i32([1, 2, 3, 0, 1]), seg_rep=i32([0, 1, 1, 0, 1]),
+             rep_ptr=i32([0, 2, 4]), rep_region=i32([0, 2, 1, 0]), kept=np.arange(2))
+    out = []
+    for mode in ('1', '0'):
+        monkeypatch.setenv('IGM_SPRITE_TABLES', mode)
+        out.append(sprite.rg2_select(xyz, copy_ptr, copy_idx, t, 7, return_rg2=True))
     for a, b in zip(*out):
         assert np.array_equal(bits(a) if a.dtype == np.float32 else a, bits(b) if b.dtype == np.float32 else b)
 

@@ -26,25 +26,26 @@ def _free_port():
     return port
 
 
-def _inputs():
+def _inputs(nstruct=32):
     pop = np.load(os.path.join(GOLDEN, 'demo_population.npz'))
     hic = np.load(os.path.join(GOLDEN, 'demo_hic_pairs.npz'))
     keep = np.where(hic['p'] >= 0.05)[0][:3001]
     pairs = make_pairs(hic['i'][keep], hic['j'][keep], hic['p'][keep].astype(np.float64), np.zeros(len(keep)))
-    xyz_sm = np.ascontiguousarray(pop['coordinates'][:, :32].transpose(1, 0, 2))  # (S, nbead, 3) struct-major
+    xyz_sm = np.ascontiguousarray(pop['coordinates'][:, :nstruct].transpose(1, 0, 2))  # (S, nbead, 3) struct-major
     return pop, pairs, xyz_sm
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, nstruct=32):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        pop, pairs, xyz_sm = _inputs()
+        pop, pairs, xyz_sm = _inputs(nstruct)
         S = xyz_sm.shape[0]
         s0, s1 = pipeline.shard(S, rank, world)
         local = torch.from_numpy(xyz_sm[s0:s1].copy())
-        full = pipeline.gather_population(local).numpy()
+        counts = [b - a for a, b in (pipeline.shard(S, r, world) for r in range(world))]
+        full = pipeline.gather_population(local, counts=counts).numpy()
         assert np.array_equal(full, xyz_sm)
         bead_major = np.ascontiguousarray(full.transpose(1, 0, 2))
         combos = pipeline.pair_combos(pairs, pop['copy_ptr'], pop['chrom'][:len(pop['copy_ptr']) - 1])
@@ -94,12 +95,14 @@ def test_weighted_pair_shards_balance_combinations():
     assert [pipeline.shard_weighted([4], r, 2) for r in range(2)] == [(0, 1), (1, 1)]
 
 
-@pytest.mark.parametrize('world', [2, 4])
-def test_multi_rank_astep_rows_equal_single_rank(tmp_path, world):
+@pytest.mark.parametrize('world,nstruct', [(2, 32), (4, 32), (3, 10)])
+def test_multi_rank_astep_rows_equal_single_rank(tmp_path, world, nstruct):
+    """(3, 10): a population that does not split evenly (4/3/3 structures per rank): the
+    padded all-gather gives the same population, and the rows equal one rank's."""
     out = str(tmp_path / 'rows.npy')
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, nstruct), nprocs=world, join=True)
     got = np.load(out)
-    pop, pairs, xyz_sm = _inputs()
+    pop, pairs, xyz_sm = _inputs(nstruct)
     ref, _ = oracle.actdist(np.ascontiguousarray(xyz_sm.transpose(1, 0, 2)), pop['radii'], pop['copy_ptr'],
                             pop['copy_idx'], pop['chrom'], pairs, 2.0, 1)
     assert got.tobytes() == ref.tobytes()

@@ -26,8 +26,9 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize('world', [2, 4])
+@pytest.mark.parametrize('world', [2, 3, 4])
 def test_gpu_ranks_equal_one_rank(tmp_path, world):
+    """(world 3: 8 structures split 2/3/3 -- uneven shards, padded all-gather)"""
     env = dict(os.environ, IGM_DIST_OUT=str(tmp_path), OMP_NUM_THREADS='2')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=%d' % world,
            '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'dist_am_worker.py')]

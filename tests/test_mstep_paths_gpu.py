@@ -195,6 +195,53 @@ def test_gpu_200kb_small_list_capacity_forces_match_oracle(ms, model200):
     assert np.linalg.norm(err) <= 1e-5 * np.linalg.norm(np.linalg.norm(fo, axis=2))
 
 
+def _with_env(env, fn):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_gpu_200kb_split_sort_equals_lds_sort(ms, model200):
+    """The population engine's list builds sort the slots by cell, ids ascending inside a
+    cell.  The split sort (pop_grid/count/scan/scatter/rank: several workgroups per flagged
+    structure, counts in HBM, the default) and the single-workgroup LDS sort
+    (IGM_POP_SORT=0) give the same slot order, so a protocol run is bitwise the same on
+    both; so is the split sort with one structure slot in the build grids
+    (IGM_POP_BUILD_SLOTS=1: every block loops over the flagged structures), with 3
+    structure groups, and its own rerun."""
+    atoms, poly, prm, ptr, sb, x = model200
+    n = 6
+    x6 = np.concatenate([x] * 3)
+    rng = np.random.default_rng(77)
+    x6[:, :atoms.nbead] += rng.normal(0, 30.0, (n, atoms.nbead, 3)).astype(np.float32)
+    per = [sb[ptr[s % 2]:ptr[s % 2 + 1]] for s in range(n)]
+    ptr6, sb6 = M.concat_bonds(per)
+    p = json.loads(json.dumps(F.DEMO_PROTOCOL))
+    p['custom_annealing_protocol']['mdsteps'] = [60, 80, 80, 60]
+    p['custom_annealing_protocol']['relax']['mdsteps'] = 20
+    prm6 = M.params_from_cfg({'optimization': {'optimizer_options': p}}, [((5500.0,) * 3, 1.0)])
+    seeds = M.lammps_seeds(6535, list(range(n)), 3)
+
+    def run():
+        return ms.run(prm6, x6, atoms.radii, atoms.flags, poly, ptr6, sb6, seeds)
+    xs, is_ = run()
+    xl, il = _with_env({'IGM_POP_SORT': '0'}, run)
+    x1, i1 = _with_env({'IGM_POP_BUILD_SLOTS': '1', 'IGM_POP_GROUPS': '3'}, run)
+    xr, ir = run()
+    assert np.all(is_['nrebuild'] > 10)  # many list builds
+    for xo, io in ((xl, il), (x1, i1), (xr, ir)):
+        assert np.array_equal(xs, xo)
+        assert is_.tobytes() == io.tobytes()
+
+
 @pytest.mark.parametrize('engine', ['lds', 'hbm'])
 def test_gpu_retired_engine_flag_is_rejected(demo, ms, engine):
     """params flag 0x4 (round 3's domain-decomposed engine) is retired: igm_mstep_run returns

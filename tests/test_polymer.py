@@ -120,3 +120,21 @@ def test_gpu_polymer_assign_edge_cases(data):
         PL.assign(crd, e, p, np.random.RandomState(9), loci=[3007])  # i + 1 out of range
     _, nn = PL.assign(crd, e, p, np.random.RandomState(9), loci=np.zeros(0, np.int32))
     assert nn.shape == (0, 37)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('S', [5000, 10000])
+def test_gpu_polymer_assign_large_populations(S):
+    """Populations past the LDS-resident kernel's rank sort (S = 10000: distances and bin
+    histograms in HBM, ranks counted per structure) and just inside it (S = 5000): a
+    lattice population where many distances tie, bit-exact against the oracle."""
+    rng = np.random.default_rng(S)
+    crd = np.round(rng.normal(0.0, 3.0, (6, S, 3))).astype(np.float32)
+    e = np.linspace(1.0, 12.0, 40)
+    p = np.random.RandomState(2).rand(40)
+    p /= p.sum()
+    loci, nn, dist = PL.assign(crd, e, p, np.random.RandomState(11), loci=np.arange(5, dtype=np.int32),
+                               return_dists=True)
+    o = OA.polymer_assign(crd, loci, e, p, np.random.RandomState(11))
+    assert len(np.unique(dist[0])) < S // 4  # ties decided by structure order
+    assert nn.tobytes() == o.tobytes()
