@@ -59,6 +59,8 @@ def parse():
     ap.add_argument('--protocol-scale', type=float, default=1.0,
                     help='scale the MD step counts (only for smoke tests; the metric needs 1.0)')
     ap.add_argument('--no-c', action='store_true', help='skip the config C (200 kb) block of the N=1 line')
+    ap.add_argument('--no-mstep-de', action='store_true',
+                    help='skip the N=1 line\'s configuration D/E M-step blocks and the frustrated shard')
     ap.add_argument('--c-steps', type=int, default=1, help='timed A/M iterations of the config C block')
     ap.add_argument('--c-total', type=int, default=None,
                     help='config C population split over the ranks (default 1000: the metric\'s workload)')
@@ -369,11 +371,151 @@ def bench_shard(args, dev):
             'ms_per_step': r['ms_per_step'], 'anneal_ms': b['anneal_ms'], 'cg_ms': b['cg_ms'],
             'astep_ms': b['astep_ms'], 'mstep_ms': b['mstep_ms'], 'mean_rebuilds': b['mean_rebuilds'],
             'median_final_energy_per_bead': b['median_final_energy_per_bead'], 'roofline_frac': r['roofline']['frac'],
-            'projected_8gpu_structures_per_s': 8.0 * args.c_shard * 1000.0 / r['ms_per_step'],
+            'mstep_bound_projection_8gpu_structures_per_s': 8.0 * args.c_shard * 1000.0 / r['ms_per_step'],
             'note': 'one GPU running the %d-structure shard each of 8 GPUs owns in the pop=1000 north-star run; '
-                    'the projection (8 x shard / A/M iteration time) leaves out the population all-gather and the '
-                    'A-step pair split over 8 ranks (ms-scale against the ~%.0f s M-step)'
+                    'mstep_bound_projection = 8 x shard / its A/M iteration time: an M-step-bound projection, NOT a '
+                    'measurement -- it leaves out the population all-gather and counts the shard\'s own A-step in '
+                    'place of 1/8 of the pop=1000 A-step (both ms-scale against the ~%.0f s M-step)'
                     % (args.c_shard, b['mstep_ms'] / 1000.0)}
+
+
+def _evaluations(prm):
+    """force evaluations of one anneal per structure (AMIteration.anneal_evaluations)"""
+    n = 0
+    for k in range(prm.nstages):
+        if prm.relax_steps > 0:
+            n += prm.relax_steps + 1
+        n += prm.mdsteps[k] + 1
+    return n
+
+
+def _mstep_timed(run, ctx):
+    """run() = one M-step launch sequence (anneal + CG [+ violation records]) with host
+    inputs/outputs, after a device sync; its wall time and the engine's HIP-event times"""
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return out, dt, {k: ctx.kernel_ms(k) for k in ('anneal', 'cg', 'violations')}
+
+
+def bench_mstep_de(args, dev, config, n):
+    """Configurations D and E (BASELINE.json configs[3], configs[4]) through the M-step on
+    the n-structure per-GPU shard of the pop=1000 8-GPU run: 200 kb diploid (the population
+    engine), the restraints of ModelingStep.task (ModelingStep.py:402-503) assembled by
+    igm_amd.assemble from igm_amd.workloads' specs -- D: lamina DamID (its A-step,
+    igm_damid_select membership, the k < 0 envelope, lammps.py:292-310) on the ellipsoidal
+    nucleus; E: SPRITE centroid slots + bounds, FISH radial/pair bounds (their A-steps) and
+    the imaged nucleus map (per-bead volume lookups) -- both with 16.5k frustrated Hi-C-like
+    contacts per structure; full demo protocol.  One A/M iteration, timed in its parts:
+    A-steps (the spec's GPU A-steps and host reductions), assembly (host), M-step (anneal +
+    CG + violation records, host arrays in and out: PCIe included)."""
+    import types
+    from igm_amd import _lib, assemble as A, model as M, volume as V, workloads as W
+    ctx = _lib.context(dev.index or 0)
+    progress('config %s M-step (%d structures)' % (config, n))
+    pop = W.population(config, n, first_sid=0)
+    sids = np.arange(n)
+    vol = None
+    t0 = time.perf_counter()
+    if config == 'D':
+        spec = W.spec_D(pop, n, args.protocol_scale, ctx)
+    else:
+        vol = V.sphere_map(5500.0, 100.0)
+        spec = W.spec_E(pop, n, args.protocol_scale, ctx, vol)
+    t1 = time.perf_counter()
+    idx = types.SimpleNamespace(radii=pop['radii'], chrom=pop['chrom'], copy=pop['copy'], copy_ptr=pop['copy_ptr'],
+                                copy_idx=pop['copy_idx'])
+    b = A.build(pop['xyz'], sids, idx, spec, ctx)
+    t2 = time.perf_counter()
+    seeds = M.lammps_seeds(6535, sids, 1)
+    try:
+        (xg, info, st), dt, kms = _mstep_timed(lambda: A.run(b, seeds, 0.05, ctx), ctx)
+    finally:
+        if vol is not None:
+            V.stage(ctx, [])
+    nbonds = np.diff(b.ptr) + len(b.poly)
+    per_eval = float(np.sum(76.0 * b.natom + 16.0 * nbonds))
+    abytes = per_eval * _evaluations(b.prm)
+    achieved = abytes / (kms['anneal'] * 1e-3) / 1e9
+    mix = {}
+    for c in range(len(b.names)):
+        nm = b.names[c] if isinstance(b.names[c], str) or b.names[c] is None else b.names[c][0]
+        if nm is None:
+            continue
+        if c < 5:
+            cnt = int(np.count_nonzero(b.bcls == c)) + (len(b.poly) * n if c == M.CLASS_POLYMER else 0)
+            mix[nm] = cnt / n
+    if b.flags.ndim == 2 and config == 'D':
+        mix['Damid lamina members'] = float(np.count_nonzero(b.flags[:, :b.nbead] & (_lib.IGM_ATOM_ENV0 << 1))) / n
+    if config == 'E':
+        mix['SPRITE centroid slots (active mean)'] = float(np.mean(b.active))
+    out = {
+        'workload': '%s: 200 kb diploid (29 838 beads), %d structures (the per-GPU shard of pop=1000 at 8 GPUs), %s, '
+                    'demo protocol%s' % (config, n, 'Hi-C-like contacts + lamina DamID (k<0 envelope) + ellipsoidal '
+                                         'nucleus' if config == 'D' else 'Hi-C-like contacts + SPRITE + FISH + imaged '
+                                         'nuclear-body map (volumetric restraint)',
+                                         '' if args.protocol_scale == 1.0 else ' x%g (NOT the metric)'
+                                         % args.protocol_scale),
+        'value': n / dt, 'unit': 'structures/s (M-step)', 'nstruct': n, 'natom': int(b.natom),
+        'mstep_s': dt, 'astep_s': t1 - t0, 'assemble_s': t2 - t1, 'iteration_s': t1 - t0 + (t2 - t1) + dt,
+        'anneal_ms': kms['anneal'], 'cg_ms': kms['cg'], 'violations_ms': kms['violations'],
+        'restraints_per_structure': mix,
+        'roofline': {'bound': 'hbm', 'kernel': 'population engine (anneal)', 'achieved': achieved,
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                     'algorithmic_bytes_per_launch': abytes, 'avg_launch_ms': kms['anneal']},
+        'median_final_energy_per_bead': float(np.median(info['final_energy'])) / b.nbead,
+        'mean_rebuilds': float(np.mean(info['nrebuild'])),
+        'note': 'value = structures / M-step wall time (anneal + CG + violation records, host arrays over PCIe); '
+                'iteration_s adds the A-steps and the host assembly of this configuration',
+    }
+    del xg, st, b
+    return out
+
+
+def bench_frustrated(args, dev, n, ncontacts=700):
+    """The north-star shard on FRUSTRATED restraints (tests/test_configC_gpu.py's stage-wise
+    recipe): a 200 kb population's A-step bonds after one warmup A/M iteration plus
+    `ncontacts` random long-range contacts per structure that cannot all be met, so the final
+    energies stay far from zero (the satisfiable synthetic .hcs anneals to ~1e-11 per bead).
+    Times the M-step (anneal + CG) of those n structures, full protocol."""
+    import torch
+    from igm_amd import model as M, mstep, workloads as W
+    from igm_amd._lib import bond_dtype
+    from igm_amd.pipeline import AMIteration
+    progress('config C frustrated shard (%d structures)' % n)
+    ca = argparse.Namespace(**vars(args))
+    ca.config, ca.nstruct, ca.sigma = 'C', n, 0.01
+    inp = build_inputs(ca, 0, first=0)
+    pop = inp['pop']
+    it = AMIteration(dev, inp['xyz'], inp['atoms'], inp['chrom'], pop['copy_ptr'], pop['copy_idx'], inp['pairs'],
+                     inp['prm'], inp['poly'], first_sid=0)
+    it.step()
+    it.astep()
+    it.select()
+    torch.cuda.synchronize(dev)
+    ptr = it.hic_ptr.cpu().numpy()
+    hic = it.hic_bonds.cpu().numpy().view(bond_dtype)[:ptr[-1]]
+    x0 = it.xyz.cpu().numpy()
+    atoms = inp['atoms']
+    per = [np.concatenate([hic[ptr[s]:ptr[s + 1]], W.random_contacts(atoms.radii, atoms.nbead, 0, ncontacts, 7000 + s)])
+           for s in range(n)]
+    sptr, sb = M.concat_bonds(per)
+    seeds = M.lammps_seeds(it.seed, it.sids, it.step_no)
+    ctx = it.ctx
+    del it
+    torch.cuda.empty_cache()
+    (xg, info), dt, kms = _mstep_timed(lambda: mstep.run(inp['prm'], x0, atoms.radii, atoms.flags, inp['poly'], sptr,
+                                                         sb, seeds, ctx=ctx), ctx)
+    return {'value': n / dt, 'unit': 'structures/s (M-step)', 'nstruct': n, 'mstep_s': dt,
+            'anneal_ms': kms['anneal'], 'cg_ms': kms['cg'],
+            'bonds_per_structure': float(sptr[-1]) / n, 'extra_contacts_per_structure': ncontacts,
+            'median_final_energy_per_bead': float(np.median(info['final_energy'])) / atoms.nbead,
+            'mean_rebuilds': float(np.mean(info['nrebuild'])),
+            'note': 'A-step bonds + %d random long-range contacts per structure (frustrated); M-step = anneal + CG, '
+                    'host arrays over PCIe' % ncontacts}
 
 
 def bench_asteps_de(args, ctx):
@@ -556,7 +698,7 @@ def main():
     score = it.violation_score()
     info = it.info_host()
     nrows, nbonds, S_local, npairs, npairs_total = int(it.nrows), it.nbonds, it.S_local, it.npairs, it.npairs_total
-    de = cblock = astep_cpu = cpu = None
+    de = cblock = astep_cpu = cpu = mde = None
     if want_cpu:
         progress('CPU baselines of config %s' % args.config)
         nth, _, _ = host_threads(args)
@@ -571,6 +713,15 @@ def main():
         cblock = bench_config_c(args, dev, world, rank, local, backend)
         if world == 1 and args.c_shard > 0 and args.c_shard != args.c_total:
             cblock['shard%d' % args.c_shard] = bench_shard(args, dev)
+            if not args.no_mstep_de:
+                cblock['shard%d_frustrated' % args.c_shard] = bench_frustrated(args, dev, args.c_shard)
+                torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and args.config == 'B' and not args.no_mstep_de:
+        n = args.c_shard if args.c_shard > 0 else 125
+        mde = {}
+        for cfg in ('D', 'E'):
+            mde['config_%s' % cfg] = bench_mstep_de(args, dev, cfg, n)
+            torch.cuda.empty_cache()
     ms_per_step = 1000.0 * dt / max(args.steps, 1)
     total = S_local * world
     value = total * args.steps / dt
@@ -606,6 +757,7 @@ def main():
             'astep_pairs_per_s': float(npairs) / (kms['actdist'] * 1e-3),
             'config_C': cblock,
             'asteps_DE': de,
+            'mstep_DE': mde,
             'breakdown': {'astep_ms': 1000 * float(np.mean(astep_s)), 'mstep_ms': 1000 * float(np.mean(mstep_s)),
                           'anneal_ms': a_ms, 'cg_ms': kms['cg'],
                           'actdist_ms': kms['actdist'], 'actdist_select_ms': kms['actdist_select'],

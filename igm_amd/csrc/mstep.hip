@@ -1492,6 +1492,7 @@ struct PopArgs {
     // structure instead of one 1024-thread workgroup holding the grid in LDS):
     int* ccnt;           // (B, kPopCntStride) cell counts; zero between builds (the scan clears them)
     int* tid;            // (B, ldn) atom ids scattered into their cells (before the in-cell rank)
+    int* ctot;           // (B, 8) cells counted per scan chunk (zero between builds: the scatter clears them)
 };
 
 // one Verlet list of the engine (the inner one, or the outer one of two-level lists)
@@ -1678,7 +1679,8 @@ __global__ void __launch_bounds__(kPopBS) pop_integrate_kernel(PopArgs A, PopSte
 // order is x-fastest, so an x run of cells stays one slot range, and a slot's list build
 // visits only the x cells its cut_list sphere meets in each row), at most A.ccap cells.
 // Stored to gp (lo[3], inv[3]) and gn (nb[3], x reach); sg/sn get lo, inv and nb.
-__device__ __forceinline__ void pop_grid_of(const PopArgs& A, int s, const float (&mm)[6], float* sg, int* sn) {
+__device__ __forceinline__ void pop_grid_of(const PopArgs& A, int s, const float (&mm)[6], float* sg, int* sn,
+                                            bool store = true) {
     float ext[3], vol = 1.0f;
     const float cut = A.P.cut_list;
 #pragma unroll
@@ -1699,16 +1701,18 @@ __device__ __forceinline__ void pop_grid_of(const PopArgs& A, int s, const float
         if (nbv[d] < 1) nbv[d] = 1;
     }
     // x cells a pair within cut_list can be apart (the cell walk's x reach)
-    gn[3] = ext[0] > 0.0f ? max(1, (int)ceilf(cut * (float)nbv[0] / ext[0] * 1.00001f)) : 1;
+    if (store) gn[3] = ext[0] > 0.0f ? max(1, (int)ceilf(cut * (float)nbv[0] / ext[0] * 1.00001f)) : 1;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         const int nbd = nbv[d];
         sg[d] = -mm[d];
         sg[3 + d] = ext[d] > 0.0f ? (float)nbd / ext[d] : 0.0f;
         sn[d] = nbd;
-        gp[d] = sg[d];
-        gp[3 + d] = sg[3 + d];
-        gn[d] = nbd;
+        if (store) {
+            gp[d] = sg[d];
+            gp[3 + d] = sg[3 + d];
+            gn[d] = nbd;
+        }
     }
 }
 
@@ -1956,111 +1960,123 @@ inline int pop_sort_cells(int natom) {
 static_assert(kPopCells < 65536, "cell ids are packed in 16 bits");
 
 // ---- The split sort: the same slot order as pop_sort_kernel (same grid, same cells, ids
-// ascending inside a cell), built by several 256-thread workgroups per flagged structure
-// over the compacted list of flagged structures, with the counts and ids in HBM/L2 instead
-// of one CU's LDS.  pop_sort_kernel holds 124 KB of LDS for ~200 us per flagged structure
-// (one workgroup's chain of dependent LDS round trips); at 125 structures per GPU ~10 such
-// workgroups sit on every step's critical path, and at pop = 1000 their LDS keeps the other
-// structure group's kernels off the CUs they occupy (profiles/r05_ab).
-//   pop_grid     one wave per structure: flagged ones get their grid and a flist entry
-//   pop_count    per slot: its cell, and its arrival rank there (global atomic), key = c << 16 | rank
-//   pop_scan     per flagged structure: cell offsets (exclusive scan), counts cleared, parity flipped
+// ascending inside a cell), built by several workgroups per flagged structure with the
+// counts and ids in HBM/L2 instead of one CU's LDS (pop_sort_kernel holds 124 KB of LDS
+// for ~200 us per flagged structure, which keeps the other structure group's kernels off
+// that CU, profiles/r05_ab).
+//   pop_count    every slot of every flagged structure: the grid (each block from the bbox
+//                partials; block 0 stores it and the flist entry), the slot's cell, its
+//                arrival rank there (global atomic), key = c << 16 | rank; chunk totals
+//   pop_scan     per flagged structure and chunk of kScanChunk cells: cell offsets
+//                (exclusive scan from the chunk totals before it), counts cleared, parity flipped
 //   pop_scatter  per slot: its atom id at its cell's first slot + arrival rank
 //   pop_rank     per slot: new slot = cell's first slot + ids of the cell below its own
 // The arrival ranks differ run to run; the in-cell order (ascending ids) does not.
-// Build kernels over the flagged structures run a grid of `per` structure slots x nbs
-// blocks, and block b takes flagged structures b / nbs, + per, ... (*nflag of them).
-__global__ void __launch_bounds__(256) pop_grid_kernel(PopArgs A, int fp) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, s = blockIdx.x * 4 + w;
-    if (s >= A.cm.nstruct || !A.flag[fp][s]) return;  // (wave-uniform)
-    const float* bp = A.bbp + (size_t)s * A.nbs * 6;
-    float mm[6];
-#pragma unroll
-    for (int d = 0; d < 6; ++d) mm[d] = -3.0e38f;
-    for (int b = lane; b < A.nbs; b += 64)
-#pragma unroll
-        for (int d = 0; d < 6; ++d) mm[d] = fmaxf(mm[d], bp[b * 6 + d]);
-#pragma unroll
-    for (int d = 0; d < 6; ++d) mm[d] = wave_max_f32(mm[d]);
-    if (lane == 0) {
-        A.flist[atomicAdd(A.nflag, 1)] = s;
-        float sg[6];
-        int sn[3];
-        pop_grid_of(A, s, mm, sg, sn);
-    }
-}
+// The kernels after pop_count run a grid of `per` structure slots x nbs blocks, and block
+// b takes flagged structures b / nbs, + per, ... (*nflag of them).
+constexpr int kScanLog = 13, kScanChunk = 1 << kScanLog, kScanChunks = 8;  // 8 x 8192 >= kPopCells
+static_assert(kScanChunk * kScanChunks >= kPopCells, "the scan chunks cover every cell");
 
-__global__ void __launch_bounds__(kPopBS) pop_count_kernel(PopArgs A) {
-    const int nf = *A.nflag, per = gridDim.x / A.nbs, i = (blockIdx.x % A.nbs) * kPopBS + threadIdx.x;
-    if (i >= A.cm.natom) return;
-    for (int k = blockIdx.x / A.nbs; k < nf; k += per) {
-        const int s = A.flist[k];
+__global__ void __launch_bounds__(kPopBS) pop_count_kernel(PopArgs A, int fp) {
+    __shared__ float sgl[6];
+    __shared__ int snb[3], scc[kScanChunks];
+    const int s = blockIdx.x / A.nbs, blk = blockIdx.x % A.nbs, t = threadIdx.x, i = blk * kPopBS + t;
+    if (s >= A.cm.nstruct || !A.flag[fp][s]) return;  // (block-uniform)
+    if (t < kScanChunks) scc[t] = 0;
+    if (t < 64) {  // the structure's bead bbox from the blocks' partials (max: exact in any order)
+        const float* bp = A.bbp + (size_t)s * A.nbs * 6;
+        float mm[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) mm[d] = -3.0e38f;
+        for (int b = t; b < A.nbs; b += 64)
+#pragma unroll
+            for (int d = 0; d < 6; ++d) mm[d] = fmaxf(mm[d], bp[b * 6 + d]);
+#pragma unroll
+        for (int d = 0; d < 6; ++d) mm[d] = wave_max_f32(mm[d]);
+        if (t == 0) {
+            float sg[6];
+            int sn[3];
+            pop_grid_of(A, s, mm, sg, sn, blk == 0);
+            if (blk == 0) A.flist[atomicAdd(A.nflag, 1)] = s;
+#pragma unroll
+            for (int d = 0; d < 6; ++d) sgl[d] = sg[d];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) snb[d] = sn[d];
+        }
+    }
+    __syncthreads();
+    if (i < A.cm.natom) {
+        const float lo[3] = {sgl[0], sgl[1], sgl[2]}, inv[3] = {sgl[3], sgl[4], sgl[5]};
+        const int nb[3] = {snb[0], snb[1], snb[2]};
         const size_t base = (size_t)s * A.cm.ldn;
-        const float* gp = A.gp + (size_t)s * 8;
-        const int* gn = A.gn + (size_t)s * 8;
-        const float lo[3] = {gp[0], gp[1], gp[2]}, inv[3] = {gp[3], gp[4], gp[5]};
-        const int nb[3] = {gn[0], gn[1], gn[2]};
         const float4 p = A.buf[A.par[s]].pos[base + i];
         const int c = p.w >= 0.0f ? pop_cell_index(p.x, p.y, p.z, lo, inv, nb) : pop_ncell(nb);
         const int r = atomicAdd(A.ccnt + (size_t)s * kPopCntStride + c, 1);
-        A.remap[base + i] = (c << 16) | r;
+        atomicAdd(&scc[c >> kScanLog], 1);  // (the chunk totals: one global add per block and chunk,
+        A.remap[base + i] = (c << 16) | r;   // not per slot -- a few words take every slot's add)
     }
+    __syncthreads();
+    if (t < kScanChunks && scc[t]) atomicAdd(A.ctot + (size_t)s * kScanChunks + t, scc[t]);
 }
 
 // exclusive scan of the counts of cells 0..ncell (the last one the non-bead run) into the
-// cell offsets (cell[ncell + 1] = N), 8 cells per thread and tile; counts cleared behind
+// cell offsets (cell[ncell + 1] = N): one workgroup per (flagged structure, chunk of
+// kScanChunk cells), 8 cells per thread, the chunk's base from the chunk totals before it;
+// the counts cleared behind
 template <int NT>
 __global__ void __launch_bounds__(NT) pop_scan_kernel(PopArgs A) {
+    static_assert(8 * NT == kScanChunk, "one tile per chunk");
     __shared__ int wsum[NT / 64];
-    const int nf = *A.nflag, t = threadIdx.x, lane = t & 63, w = t >> 6;
-    for (int k = blockIdx.x; k < nf; k += gridDim.x) {
+    const int nf = *A.nflag, t = threadIdx.x, lane = t & 63, w = t >> 6, ch = blockIdx.x % kScanChunks;
+    for (int k = blockIdx.x / kScanChunks; k < nf; k += gridDim.x / kScanChunks) {
         const int s = A.flist[k];
         const int* gn = A.gn + (size_t)s * 8;
         const int n = gn[0] * gn[1] * gn[2] + 1;  // cells and the non-bead run
+        const int c0 = ch * kScanChunk;
+        if (c0 >= n) continue;  // (block-uniform)
+        const int* ct = A.ctot + (size_t)s * kScanChunks;
+        int run = 0;
+        for (int q = 0; q < ch; ++q) run += ct[q];
         int4* cnt = reinterpret_cast<int4*>(A.ccnt + (size_t)s * kPopCntStride);
         int* cg = A.cell + (size_t)s * kPopCells;
-        int run = 0;  // offsets of the tiles before (block-uniform)
-        for (int c0 = 0; c0 < n; c0 += 8 * NT) {
-            const int c = c0 + 8 * t;
-            int4 a = make_int4(0, 0, 0, 0), b = make_int4(0, 0, 0, 0);
-            if (c < n) {  // (the stride rounds the rows to 4: c + 4 < kPopCntStride)
-                a = cnt[c >> 2];
-                b = c + 4 < n ? cnt[(c >> 2) + 1] : make_int4(0, 0, 0, 0);
-            }
-            const int v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-            int sum = 0;
+        const int c = c0 + 8 * t;
+        int4 a = make_int4(0, 0, 0, 0), b = make_int4(0, 0, 0, 0);
+        if (c < n) {  // (the stride rounds the rows to 4: c + 4 < kPopCntStride)
+            a = cnt[c >> 2];
+            b = c + 4 < n ? cnt[(c >> 2) + 1] : make_int4(0, 0, 0, 0);
+        }
+        const int v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        int sum = 0;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) sum += v[u];
-            int incl = sum;
+        for (int u = 0; u < 8; ++u) sum += v[u];
+        int incl = sum;
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int y = __shfl_up(incl, off);
-                if (lane >= off) incl += y;
-            }
-            if (lane == 63) wsum[w] = incl;
-            __syncthreads();
-            int ex = run + incl - sum, tile = 0;
-            for (int q = 0; q < NT / 64; ++q) {
-                ex += q < w ? wsum[q] : 0;
-                tile += wsum[q];
-            }
-            if (c < n) {
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        int ex = run + incl - sum, tile = 0;
+        for (int q = 0; q < NT / 64; ++q) {
+            ex += q < w ? wsum[q] : 0;
+            tile += wsum[q];
+        }
+        if (c < n) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    if (c + u < n) cg[c + u] = ex;
-                    ex += v[u];
-                }
-                const int4 z = make_int4(0, 0, 0, 0);
-                cnt[c >> 2] = z;
-                if (c + 4 < n) cnt[(c >> 2) + 1] = z;
+            for (int u = 0; u < 8; ++u) {
+                if (c + u < n) cg[c + u] = ex;
+                ex += v[u];
             }
-            run += tile;
-            __syncthreads();  // (wsum reused by the next tile)
+            const int4 z = make_int4(0, 0, 0, 0);
+            cnt[c >> 2] = z;
+            if (c + 4 < n) cnt[(c >> 2) + 1] = z;
         }
         if (t == 0) {
-            cg[n] = run;  // = N
-            A.par[s] ^= 1;  // the slot order being built is the other buffer's
+            if (c0 + kScanChunk >= n) cg[n] = run + tile;  // = N (the chunk holding the last cell)
+            if (ch == 0) A.par[s] ^= 1;  // the slot order being built is the other buffer's
         }
+        __syncthreads();  // (wsum reused by the next structure)
     }
 }
 
@@ -2069,6 +2085,7 @@ __global__ void __launch_bounds__(kPopBS) pop_scatter_kernel(PopArgs A) {
     if (i >= A.cm.natom) return;
     for (int k = blockIdx.x / A.nbs; k < nf; k += per) {
         const int s = A.flist[k];
+        if (i < kScanChunks) A.ctot[(size_t)s * kScanChunks + i] = 0;  // (read by the scan launch before)
         const size_t base = (size_t)s * A.cm.ldn;
         const uint32_t key = (uint32_t)A.remap[base + i];
         const int* cg = A.cell + (size_t)s * kPopCells;
@@ -3778,6 +3795,7 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     if (Q.ccnt) {
         V.ccnt = Q.ccnt + (size_t)s0 * kPopCntStride;
         V.tid = Q.tid + o;
+        V.ctot = Q.ctot + (size_t)s0 * 8;
     }
     V.flag[0] = Q.flag[0] + s0;
     V.flag[1] = Q.flag[1] + s0;
@@ -3981,7 +3999,21 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         Q.csr = (const uint32_t*)pcsr;
     }
     // the sort keeps its ids in LDS when they fit beside the cell counts (200 kb: 29 839 atoms)
-    Q.ccap = pop_sort_cells(N);
+    auto knob = [](const char* name, int dflt) {
+        const char* e = getenv(name);
+        return e ? atoi(e) : dflt;
+    };
+    // The sort: the single-workgroup LDS sort (default) or the split sort (IGM_POP_SORT=1;
+    // both give the same slot order at the same cell cap, tests/test_mstep_paths_gpu.py).
+    // Measured on config C (profiles/r06_ab): the split sort is 6 % slower at 125 structures
+    // per GPU (full protocol: anneal 16.2 s against 15.3 s) and 16 % at pop = 1000 (protocol
+    // x0.05: 6.01 s against 5.18 s): it moves the counts, ids and cell offsets through HBM/L2
+    // in four launches where the LDS sort keeps them on one CU, and at these populations the
+    // other structure group hides the LDS sort's latency.  Two-level lists and the fused
+    // engine keep the LDS sort.  The split sort's counts live in HBM, so its grids take
+    // kPopCellCap cells whatever the structure's size; the LDS sort's cap is what its LDS holds.
+    const bool split = knob("IGM_POP_SORT", 0) != 0 && !Q.two && !kPopFused;
+    Q.ccap = split ? kPopCellCap : pop_sort_cells(N);
     {  // x cells per cell side (IGM_POP_QX: A/B only)
         const char* e = getenv("IGM_POP_QX");
         Q.qx = e ? std::max(1, std::min(4, atoi(e))) : kPopQx;
@@ -3993,20 +4025,16 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                      : N <= 32 * kPopSortNT ? pop_sort_kernel<true, 32> : pop_sort_kernel<true, 0>;
     IGM_HIP_CHECK(c, hipFuncSetAttribute((const void*)sort_kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)sort_lds));
-    auto knob = [](const char* name, int dflt) {
-        const char* e = getenv(name);
-        return e ? atoi(e) : dflt;
-    };
-    // the split sort (default; IGM_POP_SORT=0: the single-workgroup LDS sort, A/B only --
-    // both give the same slot order); two-level lists and the fused engine keep the LDS sort
-    const bool split = knob("IGM_POP_SORT", 1) != 0 && !Q.two && !kPopFused;
     if (split) {
-        void *pcc, *ptd;
+        void *pcc, *ptd, *pct;
         IGM_TRY(workspace(c, "pop_ccnt", sizeof(int) * (size_t)S * kPopCntStride, &pcc));
         IGM_TRY(workspace(c, "pop_tid", sizeof(int) * SL, &ptd));
+        IGM_TRY(workspace(c, "pop_ctot", sizeof(int) * (size_t)S * 8, &pct));
         IGM_HIP_CHECK(c, hipMemsetAsync(pcc, 0, sizeof(int) * (size_t)S * kPopCntStride, c->stream));
+        IGM_HIP_CHECK(c, hipMemsetAsync(pct, 0, sizeof(int) * (size_t)S * 8, c->stream));
         Q.ccnt = (int*)pcc;
         Q.tid = (int*)ptd;
+        Q.ctot = (int*)pct;
     }
     // structure slots of the build kernels' grids (IGM_POP_BUILD_SLOTS): a block loops over
     // the flagged structures b / nbs, + slots, ..., so the grid need not cover every
@@ -4112,10 +4140,9 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                         const dim3 bgrid(std::min(ns, bslots) * Q.nbs);  // the build kernels' grid
                         hipLaunchKernelGGL(pop_integrate_kernel, grid_of(g), blk, 0, sg, V[g], st);
                         if (split) {
-                            hipLaunchKernelGGL(pop_grid_kernel, dim3((ns + 3) / 4), dim3(256), 0, sg, V[g], st.fp);
-                            hipLaunchKernelGGL(pop_count_kernel, bgrid, blk, 0, sg, V[g]);
-                            hipLaunchKernelGGL(pop_scan_kernel<1024>, dim3(std::min(ns, bslots)), dim3(1024), 0, sg,
-                                               V[g]);
+                            hipLaunchKernelGGL(pop_count_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g], st.fp);
+                            hipLaunchKernelGGL(pop_scan_kernel<kScanChunk / 8>, dim3(std::min(ns, bslots) * kScanChunks),
+                                               dim3(kScanChunk / 8), 0, sg, V[g]);
                             hipLaunchKernelGGL(pop_scatter_kernel, bgrid, blk, 0, sg, V[g]);
                             hipLaunchKernelGGL(pop_rank_kernel, bgrid, blk, 0, sg, V[g]);
                         } else {

@@ -281,8 +281,10 @@ def test_sprite_table_path_mixed_copies(monkeypatch):
     copy_ptr = np.array([0, 1, 3, 5, 7], np.int32)  # region 0: 1 copy, regions 1-3: 2 copies
     copy_idx = np.arange(7, dtype=np.int32)
     i32 = lambda a: np.asarray(a, np.int32)
+    # cluster 0: region 1 (2 copies) under the 1-copy representative region 0, regions 2 and 3
+    # under region 2; cluster 1: every segment with its representative's copies
     t = dict(seg_ptr=i32([0, 3, 5]), seg_region=i32([1, 2, 3, 0, 1]), seg_rep=i32([0, 1, 1, 0, 1]),
-             rep_ptr=i32([0, 2, 4]), rep_region=i32([0, 2, 1, 0]), kept=np.arange(2))
+             rep_ptr=i32([0, 2, 4]), rep_region=i32([0, 2, 0, 2]), kept=np.arange(2))
     out = []
     for mode in ('1', '0'):
         monkeypatch.setenv('IGM_SPRITE_TABLES', mode)

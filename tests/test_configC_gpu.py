@@ -19,7 +19,7 @@ import pytest
 
 import oracle
 import mstep_stats as MS
-from igm_amd import _lib
+import stagewise as SW
 from igm_amd import model as M
 from igm_amd import synthetic as syn
 from igm_amd._lib import pair_dtype
@@ -113,41 +113,20 @@ def test_gpu_200kb_protocol_matches_oracle_and_reruns_bitwise():
     assert np.all(io['temp'] < 1.0)
 
 
-def _paired(a, b):
-    """paired comparison of two engines on the same structures: Wilcoxon signed-rank p-value
-    and the median relative difference (a - b) / |b|"""
-    from scipy import stats
-    d = a - b
-    p = float(stats.wilcoxon(d).pvalue) if np.any(d != 0) else 1.0
-    return p, float(np.median(d / np.maximum(np.abs(b), 1e-30)))
-
-
 def test_gpu_200kb_full_protocol_stagewise_matches_oracle(heartbeat):
     """The bench's own workload at the FULL protocol (lammps.py:285-356: 4 stages, each a
     relax run and an annealing run after its own 'velocity create', 47 008 MD steps, then
-    min cg), on frustrated restraints, compared stage by stage with the fp64 oracle.
+    min cg), on frustrated restraints, compared stage by stage with the fp64 oracle, and the
+    product path's one igm_mstep_run over the whole protocol against the oracle's final
+    state (tests/stagewise.py: criteria and record).
 
     A 200 kb population runs one warmup A/M iteration on the GPU (AMIteration); from that
-    state the next iteration's A-step and selection give 16 (IGM_STAGEWISE_N) structures ~34 000
-    Hi-C bonds each, and 700 random long-range contacts per structure are added on top (restraints that
-    cannot all be met: the final energies stay far from zero instead of reaching ~1e-11 per
-    bead on the self-consistent synthetic .hcs alone).  Both engines then run the
-    protocol's segments from the same coordinates with the same velocities at every
-    'velocity create' (RanPark, oracle.velocity_create): the GPU population engine through
-    igm_mstep_md, the oracle through its fp64 MD; after each stage's annealing run the
-    energies (E_pair, E_bond, E_env per bead, f64 evaluation of each engine's state) and the
-    temperature are recorded -- the per-run thermo the reference reads back from LAMMPS
-    (lammps_io.py:6-37) -- and after the final CG (igm_mstep_run / the oracle with no MD
-    stage) the final energies and violation fractions.  Every stage's energies and the final
-    state agree by the two-sample KS test of tests/mstep_stats.py and by the paired Wilcoxon
-    signed-rank test over the n structures (both at alpha = 1e-3; the pairing removes the
-    structure-to-structure spread, so a systematic difference of a few per cent separates
-    them); the temperatures, which temp/rescale holds within its window (0.1) of the target,
-    differ by at most twice the window.  Everything is recorded in gpurun_out/configC_stagewise.json beside the
-    oracle's wall time."""
-    import time
+    state the next iteration's A-step and selection give 16 (IGM_STAGEWISE_N) structures
+    ~34 000 Hi-C bonds each, and 700 random long-range contacts per structure are added on
+    top (restraints that cannot all be met: the final energies stay far from zero instead of
+    reaching ~1e-11 per bead on the self-consistent synthetic .hcs alone).  Recorded in
+    gpurun_out/configC_stagewise.json beside the oracle's wall time."""
     import torch
-    from igm_amd import mstep
     from igm_amd.pipeline import AMIteration
     from igm_amd._lib import bond_dtype
     # 16 structures in the suite (the oracle runs one per thread on the box's 16 CPUs: 32 would
@@ -184,72 +163,9 @@ def test_gpu_200kb_full_protocol_stagewise_matches_oracle(heartbeat):
     per = [np.concatenate([hic[ptr[s]:ptr[s + 1]], MS.random_contacts(atoms.radii, atoms.nbead, 0, 700, 7000 + s)])
            for s in range(n)]
     ptr, sb = M.concat_bonds(per)
-    cap = proto['custom_annealing_protocol']
-    rlx = cap['relax']
-    mobile = np.count_nonzero((atoms.flags & _lib.IGM_ATOM_FIXED) == 0)
-    dof = 3.0 * mobile - 3.0
-    xg, xo = x0.copy(), x0.astype(np.float64)
-    stages, t_oracle = [], 0.0
-    for k in range(cap['num_steps']):
-        evf = prm.evfactor_base * cap['evfactors'][k]
-        envf = cap['envelope_factors'][k]
-        segs = [(rlx['temperature'], rlx['temperature'], rlx['max_velocity'], rlx['mdsteps']),
-                (cap['tstarts'][k], cap['tstops'][k], proto['max_velocity'], cap['mdsteps'][k])]
-        for si, (t0, t1, xmax, nst) in enumerate(segs):
-            v = np.stack([oracle.velocity_create(atoms.flags, t0, 1000 * s + 10 * k + si + 1) for s in range(n)])
-            xg, vg = mstep.md(prm, xg, v.astype(np.float32), atoms.radii, atoms.flags, poly, ptr, sb, evf, envf, t0,
-                              t1, xmax, nst)
-            t = time.perf_counter()
-            xo, vo = oracle.mstep_md(prm, xo, v, atoms.radii, atoms.flags, poly, ptr, sb, evf, envf, t0, t1, xmax,
-                                     nst, nthreads=16)
-            t_oracle += time.perf_counter() - t
-        _, eg = mstep.forces(prm, xg, atoms.radii, atoms.flags, poly, ptr, sb, evf, envf)
-        _, eo = oracle.mstep_forces(prm, xo.astype(np.float32), atoms.radii, atoms.flags, poly, ptr, sb, evf, envf)
-        rec = {}
-        for key, col in (('pair', 1), ('bond', 2), ('env', 3)):
-            rec[key] = (eg[:, col] / atoms.nbead, eo[:, col] / atoms.nbead)
-        rec['temp'] = ((vg.astype(np.float64) ** 2).sum(axis=(1, 2)) / dof, (vo ** 2).sum(axis=(1, 2)) / dof)
-        stages.append(rec)
-    prm0 = M.params_from_cfg({'optimization': {'optimizer_options': proto}}, [((5500.0,) * 3, 1.0)])
-    prm0.nstages = 0  # the final min cg alone
-    seeds = np.arange(n, dtype=np.int32) + 1
-    xg, ig = mstep.run(prm0, xg, atoms.radii, atoms.flags, poly, ptr, sb, seeds)
-    t = time.perf_counter()
-    xof, io, _ = oracle.mstep_run(prm0, xo.astype(np.float32), atoms.radii, atoms.flags, poly, ptr, sb, seeds,
-                                  nthreads=16)
-    t_oracle += time.perf_counter() - t
-    sg = MS.population_stats(ig, xg, poly, ptr, sb, atoms.nbead)
-    so = MS.population_stats(io, xof, poly, ptr, sb, atoms.nbead)
-    from scipy import stats as st
-    out = {'test': 'test_gpu_200kb_full_protocol_stagewise_matches_oracle', 'structures': n, 'oracle_threads': 16,
-           'oracle_s': t_oracle, 'bonds_per_structure': float(ptr[-1]) / n, 'stages': []}
-    ok = True
-    for k, rec in enumerate(stages):
-        row = {}
-        for key, (a, b) in rec.items():
-            ks = float(st.ks_2samp(a, b).pvalue)
-            pw, rel = _paired(a, b)
-            row[key] = {'gpu_median': float(np.median(a)), 'oracle_median': float(np.median(b)), 'ks_p': ks,
-                        'wilcoxon_p': pw, 'median_rel_diff': rel}
-            if key == 'temp':  # both thermostats hold T within the window of its target
-                row[key]['max_abs_diff'] = float(np.abs(a - b).max())
-                ok = ok and np.abs(a - b).max() <= 2.0 * prm.t_window + 1e-6
-            else:
-                ok = ok and ks > 1e-3 and pw > 1e-3
-        out['stages'].append(row)
-    final = {}
-    for key in ('pair', 'bond', 'total', 'viol_frac'):
-        ks = float(st.ks_2samp(sg[key], so[key]).pvalue)
-        pw, rel = _paired(sg[key], so[key])
-        final[key] = {'gpu_median': float(np.median(sg[key])), 'oracle_median': float(np.median(so[key])), 'ks_p': ks,
-                      'wilcoxon_p': pw, 'median_rel_diff': rel}
-        ok = ok and ks > 1e-3 and pw > 1e-3
-    out['final'] = final
-    print('[stagewise]', json.dumps(out))
-    d = os.path.join(os.environ.get('GRAFT_REPO_ROOT', ROOT), 'gpurun_out')
-    os.makedirs(d, exist_ok=True)
-    with open(os.path.join(d, 'configC_stagewise.json'), 'w') as fh:
-        json.dump(out, fh, indent=1)
+    seeds = M.lammps_seeds(6535, np.arange(n), 1)
+    ok, out, (sg, so, sp) = SW.run(prm, proto, x0, atoms.radii, atoms.flags, poly, ptr, sb, seeds, atoms.nbead,
+                                   'configC_stagewise')
     assert ok, out
     # frustrated: the compared final energies are far from zero (~40 per bead)
     assert np.median(so['total']) > 1e-2 and np.median(sg['total']) > 1e-2

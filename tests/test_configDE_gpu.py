@@ -92,3 +92,42 @@ def test_gpu_200kb_protocol_population_matches_oracle(config):
         assert b.active.min() > 0 and np.all(sg[:, names.index('Fish'), 103] > 0)
         # the map restraint is active in the initial (1.27x oversized) territories
         assert np.all(ig['einitial'] > ig['final_energy'])
+
+
+@pytest.mark.parametrize('config', ['D', 'E'])
+def test_gpu_200kb_stagewise_matches_oracle(config, heartbeat):
+    """Configurations D and E stage by stage (tests/stagewise.py, the design of config C's
+    full-protocol test): 16 structures, the demo protocol's MD steps x0.2 (9 400 per
+    structure), each stage's energies -- pair, bond, every envelope (D: the nucleus ellipsoid
+    and the k < 0 lamina DamID envelope; E: the volumetric map) -- and temperatures against
+    the fp64 oracle from the same coordinates and velocities, the final CG state and the
+    product path's whole-protocol igm_mstep_run against the oracle's final state; restraints
+    frustrated (16.5k Hi-C-like contacts per structure, 1 500 of them long-range), so the
+    final energies stay >= 1e-2 per bead.  Protocol: lammps.py:285-356; restraints:
+    ModelingStep.py:402-503."""
+    import stagewise as SW
+    from igm_amd import _lib, assemble as A, volume as V
+    n, scale = 16, 0.2
+    ctx = _lib.context(0)
+    pop = de200.population(config, n, first_sid=900)
+    vol = None
+    if config == 'D':
+        spec = de200.spec_D(pop, n, scale, ctx)
+    else:
+        vol = V.sphere_map(5500.0, 100.0)
+        spec = de200.spec_E(pop, n, scale, ctx, vol)
+    sids = np.arange(n)
+    b = A.build(pop['xyz'], sids, de200.index_of(pop), spec, ctx)
+    seeds = M.lammps_seeds(6535, 900 + sids, 2)
+    try:
+        if vol is not None:
+            oracle.set_volume(vol)
+        ok, out, (sg, so, sp) = SW.run(b.prm, spec['protocol'], b.x, b.radii, b.flags, b.poly, b.ptr, b.bonds, seeds,
+                                       b.nbead, 'config%s_stagewise' % config, ctx=ctx)
+    finally:
+        if vol is not None:
+            oracle.set_volume(None)
+            V.stage(ctx, [])
+    assert ok, out
+    assert len(out['stages'][0]) == 4 + b.prm.nenvelopes  # T1, pair, bond, temp + every envelope
+    assert np.median(so['total']) > 1e-2 and np.median(sg['total']) > 1e-2 and np.median(sp['total']) > 1e-2

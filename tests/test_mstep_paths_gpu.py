@@ -211,12 +211,11 @@ def _with_env(env, fn):
 
 def test_gpu_200kb_split_sort_equals_lds_sort(ms, model200):
     """The population engine's list builds sort the slots by cell, ids ascending inside a
-    cell.  The split sort (pop_grid/count/scan/scatter/rank: several workgroups per flagged
-    structure, counts in HBM, the default) and the single-workgroup LDS sort
-    (IGM_POP_SORT=0) give the same slot order, so a protocol run is bitwise the same on
-    both; so is the split sort with one structure slot in the build grids
-    (IGM_POP_BUILD_SLOTS=1: every block loops over the flagged structures), with 3
-    structure groups, and its own rerun."""
+    cell.  The single-workgroup LDS sort (the default) and the split sort (IGM_POP_SORT=1:
+    pop_count/scan/scatter/rank, several workgroups per flagged structure, counts in HBM)
+    give the same slot order, so a protocol run is bitwise the same on both; so is the
+    split sort with one structure slot in the build grids (IGM_POP_BUILD_SLOTS=1: every
+    block loops over the flagged structures), with 3 structure groups, and its rerun."""
     atoms, poly, prm, ptr, sb, x = model200
     n = 6
     x6 = np.concatenate([x] * 3)
@@ -232,10 +231,10 @@ def test_gpu_200kb_split_sort_equals_lds_sort(ms, model200):
 
     def run():
         return ms.run(prm6, x6, atoms.radii, atoms.flags, poly, ptr6, sb6, seeds)
-    xs, is_ = run()
-    xl, il = _with_env({'IGM_POP_SORT': '0'}, run)
-    x1, i1 = _with_env({'IGM_POP_BUILD_SLOTS': '1', 'IGM_POP_GROUPS': '3'}, run)
-    xr, ir = run()
+    xs, is_ = _with_env({'IGM_POP_SORT': '1'}, run)
+    xl, il = run()
+    x1, i1 = _with_env({'IGM_POP_SORT': '1', 'IGM_POP_BUILD_SLOTS': '1', 'IGM_POP_GROUPS': '3'}, run)
+    xr, ir = _with_env({'IGM_POP_SORT': '1'}, run)
     assert np.all(is_['nrebuild'] > 10)  # many list builds
     for xo, io in ((xl, il), (x1, i1), (xr, ir)):
         assert np.array_equal(xs, xo)
