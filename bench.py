@@ -401,6 +401,15 @@ def _mstep_timed(run, ctx):
     return out, dt, {k: ctx.kernel_ms(k) for k in ('anneal', 'cg', 'violations')}
 
 
+def _warm_prm(args, scale=0.1):
+    """the demo protocol with the MD steps x scale (x args.protocol_scale): the warmup A/M
+    iteration that takes a RandomInit population to annealed structures before the timed
+    one (the steady state of igm-run's loop, where each M-step starts from the last)"""
+    from igm_amd import model as M, workloads as W
+    proto = W.scaled_protocol(syn_protocol(), scale * args.protocol_scale)
+    return M.params_from_cfg({'optimization': {'optimizer_options': proto}}, [((5500.0,) * 3, 1.0)])
+
+
 def bench_mstep_de(args, dev, config, n):
     """Configurations D and E (BASELINE.json configs[3], configs[4]) through the M-step on
     the n-structure per-GPU shard of the pop=1000 8-GPU run: 200 kb diploid (the population
@@ -409,29 +418,35 @@ def bench_mstep_de(args, dev, config, n):
     igm_damid_select membership, the k < 0 envelope, lammps.py:292-310) on the ellipsoidal
     nucleus; E: SPRITE centroid slots + bounds, FISH radial/pair bounds (their A-steps) and
     the imaged nucleus map (per-bead volume lookups) -- both with 16.5k frustrated Hi-C-like
-    contacts per structure; full demo protocol.  One A/M iteration, timed in its parts:
-    A-steps (the spec's GPU A-steps and host reductions), assembly (host), M-step (anneal +
-    CG + violation records, host arrays in and out: PCIe included)."""
+    contacts per structure; full demo protocol.  A warmup A/M iteration (protocol x0.1) takes
+    the RandomInit territories to annealed structures; the next A/M iteration is timed in its
+    parts: A-steps (the spec's GPU A-steps and host reductions, on the warmed population),
+    assembly (host), M-step (anneal + CG + violation records, host arrays in and out: PCIe
+    included)."""
     import types
     from igm_amd import _lib, assemble as A, model as M, volume as V, workloads as W
     ctx = _lib.context(dev.index or 0)
     progress('config %s M-step (%d structures)' % (config, n))
     pop = W.population(config, n, first_sid=0)
     sids = np.arange(n)
-    vol = None
-    t0 = time.perf_counter()
-    if config == 'D':
-        spec = W.spec_D(pop, n, args.protocol_scale, ctx)
-    else:
-        vol = V.sphere_map(5500.0, 100.0)
-        spec = W.spec_E(pop, n, args.protocol_scale, ctx, vol)
-    t1 = time.perf_counter()
+    vol = V.sphere_map(5500.0, 100.0) if config == 'E' else None
     idx = types.SimpleNamespace(radii=pop['radii'], chrom=pop['chrom'], copy=pop['copy'], copy_ptr=pop['copy_ptr'],
                                 copy_idx=pop['copy_idx'])
-    b = A.build(pop['xyz'], sids, idx, spec, ctx)
-    t2 = time.perf_counter()
-    seeds = M.lammps_seeds(6535, sids, 1)
+
+    def spec_of(scale):
+        return W.spec_D(pop, n, scale, ctx) if config == 'D' else W.spec_E(pop, n, scale, ctx, vol)
     try:
+        # warmup A/M iteration (protocol x0.1) from RandomInit
+        b = A.build(pop['xyz'], sids, idx, spec_of(0.1 * args.protocol_scale), ctx)
+        xw, _, _ = A.run(b, M.lammps_seeds(6535, sids, 0), 0.05, ctx)
+        pop = dict(pop, xyz=np.ascontiguousarray(xw[:, :b.nbead]))
+        # the timed A/M iteration
+        t0 = time.perf_counter()
+        spec = spec_of(args.protocol_scale)
+        t1 = time.perf_counter()
+        b = A.build(pop['xyz'], sids, idx, spec, ctx)
+        t2 = time.perf_counter()
+        seeds = M.lammps_seeds(6535, sids, 1)
         (xg, info, st), dt, kms = _mstep_timed(lambda: A.run(b, seeds, 0.05, ctx), ctx)
     finally:
         if vol is not None:
@@ -469,7 +484,8 @@ def bench_mstep_de(args, dev, config, n):
         'median_final_energy_per_bead': float(np.median(info['final_energy'])) / b.nbead,
         'mean_rebuilds': float(np.mean(info['nrebuild'])),
         'note': 'value = structures / M-step wall time (anneal + CG + violation records, host arrays over PCIe); '
-                'iteration_s adds the A-steps and the host assembly of this configuration',
+                'iteration_s adds the A-steps and the host assembly of this configuration; timed after a warmup '
+                'A/M iteration (protocol x0.1) from RandomInit',
     }
     del xg, st, b
     return out
@@ -491,8 +507,9 @@ def bench_frustrated(args, dev, n, ncontacts=700):
     inp = build_inputs(ca, 0, first=0)
     pop = inp['pop']
     it = AMIteration(dev, inp['xyz'], inp['atoms'], inp['chrom'], pop['copy_ptr'], pop['copy_idx'], inp['pairs'],
-                     inp['prm'], inp['poly'], first_sid=0)
-    it.step()
+                     _warm_prm(args), inp['poly'], first_sid=0)
+    it.step()  # the first A/M iteration from RandomInit (protocol x0.1: relaxes the territories)
+    it.params = inp['prm']
     it.astep()
     it.select()
     torch.cuda.synchronize(dev)

@@ -8,6 +8,8 @@
 //   perm16   float4 per lane at a bijective hash of the index (each float4 once,     1 GiB
 //            the 64 lanes on 64 different lines: the force kernel's gathers)
 //   perm12   the same positions read as 12-byte b96 loads (the fill's candidates)    0.75 GiB
+//   halves   two lanes per 128-B line (2^23 lines, permuted), its two 64-B halves     256 MiB
+//   same64   two lanes per line, both in the same 64-B half                          256 MiB
 // Each kernel runs REPS times (the counters are summed per kernel name; divide by REPS).
 // Build: scripts/build_calib.sh -> igm_amd/lib/calib/gather_calib; run on the box:
 //   rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum -- igm_amd/lib/calib/gather_calib
@@ -62,6 +64,23 @@ __global__ void __launch_bounds__(kBS) perm12_kernel(const float4* __restrict__ 
     if (v.x == 12345.0f) out[g & 1023] = v.y + v.z;
 }
 
+// two lanes per 128-B line of a permuted line order: halves = the line's two 64-B halves
+// (float4 0 and 4), same64 = two float4 of one 64-B half (0 and 1).  If a gather miss makes
+// the L2 fetch its whole 128-B line, halves costs one request per line; if it fetches 64-B
+// sectors, two.  same64 is one request per line either way.
+__global__ void __launch_bounds__(kBS) halves_kernel(const float4* __restrict__ a, float* out) {
+    const unsigned g = blockIdx.x * kBS + threadIdx.x;  // g < kN / 4
+    const unsigned line = perm(g >> 1) & (kMask >> 3);
+    const float4 v = a[(line << 3) + ((g & 1) << 2)];
+    if (v.x == 12345.0f) out[g & 1023] = v.y + v.z + v.w;
+}
+__global__ void __launch_bounds__(kBS) same64_kernel(const float4* __restrict__ a, float* out) {
+    const unsigned g = blockIdx.x * kBS + threadIdx.x;
+    const unsigned line = perm(g >> 1) & (kMask >> 3);
+    const float4 v = a[(line << 3) + (g & 1)];
+    if (v.x == 12345.0f) out[g & 1023] = v.y + v.z + v.w;
+}
+
 int main() {
     float4* a;
     float* out;
@@ -78,11 +97,15 @@ int main() {
     } ks[] = {{"stream", stream_kernel, 16.0 * kN},
               {"line8", line8_kernel, 16.0 * kN},
               {"perm16", perm16_kernel, 16.0 * kN},
-              {"perm12", perm12_kernel, 12.0 * kN}};
-    const dim3 grid(kN / kBS);
+              {"perm12", perm12_kernel, 12.0 * kN},
+              {"halves", halves_kernel, 32.0 * (kN / 8)},
+              {"same64", same64_kernel, 32.0 * (kN / 8)}};
+    hipLaunchKernelGGL(stream_kernel, dim3(kN / kBS), dim3(kBS), 0, 0, a, out);  // (untimed: first-touch costs)
+    CK(hipDeviceSynchronize());
     printf("{\"reps\": %d, \"buffer_bytes\": %.0f, \"kernels\": {", REPS, 16.0 * kN);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 6; ++k) {
         float ms = 0.0f;
+        const dim3 grid(k < 4 ? kN / kBS : kN / 4 / kBS);  // (halves, same64: 2 lanes per line, every line once)
         for (int r = 0; r < REPS; ++r) {
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(ks[k].fn, grid, dim3(kBS), 0, 0, a, out);
