@@ -44,6 +44,7 @@ void igm_ctx_destroy(igm_ctx* c) {
         (void)hipEventDestroy(c->aux_ev[g]);
     }
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    for (hipEvent_t ev : c->step_ev) (void)hipEventDestroy(ev);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

@@ -33,6 +33,8 @@ struct igm_ctx {
     std::vector<hipStream_t> aux;
     std::vector<hipEvent_t> aux_ev;
     hipEvent_t fork_ev = nullptr;
+    // events ordering work between the auxiliary streams inside one call (pop_event)
+    std::vector<hipEvent_t> step_ev;
 };
 
 namespace igm {
@@ -152,6 +154,17 @@ inline int aux_streams(igm_ctx* c, int n) {
         c->aux.push_back(st);
         c->aux_ev.push_back(ev);
     }
+    return IGM_OK;
+}
+
+// event k of the context's cross-stream events (created on first use, timing disabled)
+inline int pop_event(igm_ctx* c, int k, hipEvent_t* out) {
+    while ((int)c->step_ev.size() <= k) {
+        hipEvent_t ev;
+        IGM_HIP_CHECK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->step_ev.push_back(ev);
+    }
+    *out = c->step_ev[k];
     return IGM_OK;
 }
 

@@ -5,3 +5,5 @@ cd "$(dirname "$0")/.."
 mkdir -p igm_amd/lib/calib
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o igm_amd/lib/calib/gather_calib scripts/gather_calib.hip
 echo built igm_amd/lib/calib/gather_calib
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -o igm_amd/lib/calib/gather_rate scripts/gather_rate.hip
+echo built igm_amd/lib/calib/gather_rate

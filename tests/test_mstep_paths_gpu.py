@@ -209,13 +209,15 @@ def _with_env(env, fn):
                 os.environ[k] = v
 
 
-def test_gpu_200kb_split_sort_equals_lds_sort(ms, model200):
+def test_gpu_200kb_build_variants_bitwise_equal(ms, model200):
     """The population engine's list builds sort the slots by cell, ids ascending inside a
     cell.  The single-workgroup LDS sort (the default) and the split sort (IGM_POP_SORT=1:
     pop_count/scan/scatter/rank, several workgroups per flagged structure, counts in HBM)
     give the same slot order, so a protocol run is bitwise the same on both; so is the
     split sort with one structure slot in the build grids (IGM_POP_BUILD_SLOTS=1: every
-    block loops over the flagged structures), with 3 structure groups, and its rerun."""
+    block loops over the flagged structures), with 3 structure groups, and its rerun; and so
+    is the engine without the forces of the structures not rebuilt at a step running ahead of
+    the list builds on a second stream (IGM_POP_EARLY=0: one force launch per step)."""
     atoms, poly, prm, ptr, sb, x = model200
     n = 6
     x6 = np.concatenate([x] * 3)
@@ -235,8 +237,9 @@ def test_gpu_200kb_split_sort_equals_lds_sort(ms, model200):
     xl, il = run()
     x1, i1 = _with_env({'IGM_POP_SORT': '1', 'IGM_POP_BUILD_SLOTS': '1', 'IGM_POP_GROUPS': '3'}, run)
     xr, ir = _with_env({'IGM_POP_SORT': '1'}, run)
+    xe, ie = _with_env({'IGM_POP_EARLY': '0'}, run)
     assert np.all(is_['nrebuild'] > 10)  # many list builds
-    for xo, io in ((xl, il), (x1, i1), (xr, ir)):
+    for xo, io in ((xl, il), (x1, i1), (xr, ir), (xe, ie)):
         assert np.array_equal(xs, xo)
         assert is_.tobytes() == io.tobytes()
 
