@@ -18,6 +18,11 @@ config_C block (the metric's own workload, BASELINE.json "200kb diploid pop=1000
 (all 1000 on one GPU; at 8 GPUs the 125-structure shards, the north-star run), Hi-C
 sigma 0.01, full protocol, the A-step over the whole population after one RCCL
 all-gather; c_warmup + c_steps A/M iterations between barriers, max over ranks.
+N=1 only, beside it: the 125-structure shard of config C on frustrated restraints (A-step
+bonds + 700 random long-range contacts per structure), and configurations D and E
+(BASELINE.json configs[3], configs[4]) through one M-step of the 125-structure shard
+(mstep_DE: DamID / SPRITE / FISH / volumetric-map restraints assembled by
+igm_amd.assemble, after a warmup iteration).
 CPU baselines (rank 0, N=1): the fp64 C port on the state of the first TIMED step
 (snapshot after the warmup: same coordinates, restraints, seeds), one structure per
 thread on every CPU the process may use (the affinity mask capped by the cgroup CPU
@@ -417,8 +422,9 @@ def bench_mstep_de(args, dev, config, n):
     igm_amd.assemble from igm_amd.workloads' specs -- D: lamina DamID (its A-step,
     igm_damid_select membership, the k < 0 envelope, lammps.py:292-310) on the ellipsoidal
     nucleus; E: SPRITE centroid slots + bounds, FISH radial/pair bounds (their A-steps) and
-    the imaged nucleus map (per-bead volume lookups) -- both with 16.5k frustrated Hi-C-like
-    contacts per structure; full demo protocol.  A warmup A/M iteration (protocol x0.1) takes
+    the imaged nucleus map (per-bead volume lookups) -- both with the Hi-C restraints of the
+    Hi-C A-step (actdist over the synthetic 200 kb .hcs at sigma 0.01, as config C); full
+    demo protocol.  A warmup A/M iteration (protocol x0.1) takes
     the RandomInit territories to annealed structures; the next A/M iteration is timed in its
     parts: A-steps (the spec's GPU A-steps and host reductions, on the warmed population),
     assembly (host), M-step (anneal + CG + violation records, host arrays in and out: PCIe
@@ -433,8 +439,10 @@ def bench_mstep_de(args, dev, config, n):
     idx = types.SimpleNamespace(radii=pop['radii'], chrom=pop['chrom'], copy=pop['copy'], copy_ptr=pop['copy_ptr'],
                                 copy_idx=pop['copy_idx'])
 
-    def spec_of(scale):
-        return W.spec_D(pop, n, scale, ctx) if config == 'D' else W.spec_E(pop, n, scale, ctx, vol)
+    def spec_of(scale):  # the A-steps of the configuration on the current population
+        hic = W.hic_actdist_rows(pop)
+        return (W.spec_D(pop, n, scale, ctx, hic=hic) if config == 'D' else
+                W.spec_E(pop, n, scale, ctx, vol, hic=hic))
     try:
         # warmup A/M iteration (protocol x0.1) from RandomInit
         b = A.build(pop['xyz'], sids, idx, spec_of(0.1 * args.protocol_scale), ctx)
@@ -469,9 +477,9 @@ def bench_mstep_de(args, dev, config, n):
         mix['SPRITE centroid slots (active mean)'] = float(np.mean(b.active))
     out = {
         'workload': '%s: 200 kb diploid (29 838 beads), %d structures (the per-GPU shard of pop=1000 at 8 GPUs), %s, '
-                    'demo protocol%s' % (config, n, 'Hi-C-like contacts + lamina DamID (k<0 envelope) + ellipsoidal '
-                                         'nucleus' if config == 'D' else 'Hi-C-like contacts + SPRITE + FISH + imaged '
-                                         'nuclear-body map (volumetric restraint)',
+                    'demo protocol%s' % (config, n, 'Hi-C (A-step rows, sigma 0.01) + lamina DamID (k<0 envelope) + '
+                                         'ellipsoidal nucleus' if config == 'D' else 'Hi-C (A-step rows, sigma 0.01) + '
+                                         'SPRITE + FISH + imaged nuclear-body map (volumetric restraint)',
                                          '' if args.protocol_scale == 1.0 else ' x%g (NOT the metric)'
                                          % args.protocol_scale),
         'value': n / dt, 'unit': 'structures/s (M-step)', 'nstruct': n, 'natom': int(b.natom),

@@ -14,9 +14,10 @@ bench times these workloads and tests/de200.py checks them against the oracle.
      over synthetic clusters, centroid slots and bead->centroid bounds
      (ModelingStep.py:456-480); FISH: the A-step's rank-matched radial and pair
      targets, lower/upper bounds to the centre and between copies (:482-503).
-Both carry frustrated Hi-C-like contacts (random_contacts, as actdist rows whose
-activation distance admits every structure), so the final energies balance every
-term and respond to each of them.
+The parity tests give both frustrated Hi-C-like contacts (random_contacts, as actdist rows
+whose activation distance admits every structure), so the final energies balance every
+term and respond to each of them; the bench gives them the Hi-C A-step's rows
+(hic_actdist_rows), the satisfiable restraint set of igm-run's loop.
 """
 import json
 
@@ -74,7 +75,22 @@ def population(config, n, first_sid):
     return syn.population_200kb(n, first_sid=first_sid)
 
 
-def spec_D(pop, n, scale, ctx, nlocal=15000, nlong=1500, seed=41):
+def hic_actdist_rows(pop, sigma=0.01, contact_range=2.0):
+    """the Hi-C A-step (get_actdist over the synthetic 200 kb .hcs at `sigma`, it_corr 1) on
+    this population: the activated rows ModelingStep's Hi-C restraints select from (a
+    satisfiable restraint set, as in igm-run's loop, where the frustrated random_contacts
+    are the parity tests' choice)"""
+    from . import astep
+    from ._lib import pair_dtype
+    i, j, p = syn.hic_pairs_200kb(sigma)
+    pairs = np.zeros(len(i), pair_dtype)
+    pairs['i'], pairs['j'], pairs['pwish'] = i, j, p
+    xyz_bm = np.ascontiguousarray(pop['xyz'].transpose(1, 0, 2))
+    return astep.compute_actdist(xyz_bm, pop['radii'], pop['copy_ptr'], pop['copy_idx'], pop['chrom'], pairs,
+                                 contact_range, 1)
+
+
+def spec_D(pop, n, scale, ctx, nlocal=15000, nlong=1500, seed=41, hic=None):
     from . import assemble as A
     from . import damid
     xyz_bm = np.ascontiguousarray(pop['xyz'].transpose(1, 0, 2))
@@ -85,12 +101,13 @@ def spec_D(pop, n, scale, ctx, nlocal=15000, nlong=1500, seed=41):
     return {'evfactor': 1.0, 'protocol': scaled_protocol(syn.DEMO_PROTOCOL, scale),
             'polymer': {'contact_range': 2.0, 'kspring': 1.0},
             'envelope': A.envelope_spec('ellipsoid', semiaxes=syn.ELLIPSOID_D, k=1.0),
-            'hic': {'rows': hic_rows(pop['radii'], nb, nlocal, nlong, seed), 'contact_range': 2.0, 'k': 1.0},
+            'hic': {'rows': hic_rows(pop['radii'], nb, nlocal, nlong, seed) if hic is None else hic,
+                    'contact_range': 2.0, 'k': 1.0},
             'damid': {'rows': drows, 'contact_range': DAMID_CR, 'k': 1.0}}
 
 
 def spec_E(pop, n, scale, ctx, vol, nclusters=2000, keep_best=4, nprobe=50, npair=50, nlocal=15000, nlong=1500,
-           seed=43):
+           seed=43, hic=None):
     from . import fish, sprite
     xyz_bm = np.ascontiguousarray(pop['xyz'].transpose(1, 0, 2))
     cp, ci = pop['copy_ptr'], pop['copy_idx']
@@ -113,7 +130,8 @@ def spec_E(pop, n, scale, ctx, vol, nclusters=2000, keep_best=4, nprobe=50, npai
             'polymer': {'contact_range': 2.0, 'kspring': 1.0},
             'envelope': {'shape': 'exp_map', 'k': 1.0, 'volumes': [vol], 'struct_map': None,
                          'files': ['nucleus_sphere.bin']},
-            'hic': {'rows': hic_rows(pop['radii'], nb, nlocal, nlong, seed), 'contact_range': 2.0, 'k': 1.0},
+            'hic': {'rows': hic_rows(pop['radii'], nb, nlocal, nlong, seed) if hic is None else hic,
+                    'contact_range': 2.0, 'k': 1.0},
             'sprite': {'assignment': assignment, 'indptr': indptr, 'selected': selected, 'volume_fraction': 0.2,
                        'k': 1.0},
             'fish': {'data': fd, 'rtype': 'rRpP', 'tol': 50.0, 'k': 1.0}}
