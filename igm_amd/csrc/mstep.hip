@@ -1493,10 +1493,6 @@ struct PopArgs {
     int* ccnt;           // (B, kPopCntStride) cell counts; zero between builds (the scan clears them)
     int* tid;            // (B, ldn) atom ids scattered into their cells (before the in-cell rank)
     int* ctot;           // (B, 8) cells counted per scan chunk (zero between builds: the scatter clears them)
-    // Block windows (IGM_POP_WIN): per kPopBS-slot block the three slot intervals its atoms'
-    // neighbours lie in (one per z-layer), computed by the fill at the block's list build;
-    // the force kernel stages them in LDS and reads neighbours and bond partners there
-    int* win;            // (B, nbs, 8): lo[3], len[3]
 };
 
 // one Verlet list of the engine (the inner one, or the outer one of two-level lists)
@@ -2186,120 +2182,6 @@ __device__ __forceinline__ float4 pop_ld(__amdgpu_buffer_rsrc_t r, uint32_t j) {
     return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 
-#ifndef IGM_POP_WIN_CAP
-#define IGM_POP_WIN_CAP 1400
-#endif
-// slots of a block's LDS window (16 B each: 22.4 KB).  Measured in round 5 on config C (pop =
-// 1000, IGM_POP_STATS): the three intervals of a 256-slot block hold 975-1180 slots on
-// average, at most 2 324 (hot run); past the cap the row margin shrinks and the entries
-// outside are read from HBM.
-constexpr int kWinCap = IGM_POP_WIN_CAP;
-
-struct PopWin {
-    int lo[3];   // first slot of each interval (merged, ascending)
-    int len[3];  // slots (0: unused)
-};
-
-// slot j's position: from the block's window in LDS when it lies there, else gathered
-// (the intervals are staged back to back: interval k at the total of the ones before it)
-__device__ __forceinline__ float4 pop_wld(const IGM_LDS float4* wpos, const PopWin& W, __amdgpu_buffer_rsrc_t r,
-                                          uint32_t j) {
-    const uint32_t d0 = j - (uint32_t)W.lo[0], d1 = j - (uint32_t)W.lo[1], d2 = j - (uint32_t)W.lo[2];
-    const int w = d0 < (uint32_t)W.len[0] ? (int)d0
-                  : d1 < (uint32_t)W.len[1] ? W.len[0] + (int)d1
-                  : d2 < (uint32_t)W.len[2] ? W.len[0] + W.len[1] + (int)d2 : -1;
-    float4 v = wpos[w >= 0 ? w : 0];
-    if (w < 0) v = pop_ld(r, j);
-    return v;
-}
-
-// The slot window of a block of kPopBS slots (the slots its atoms' neighbours can be in):
-// in the slot order of the build (cells x-fastest), the 27 cells around any cell c of the
-// block's cells [c0, c1] lie in the three cell ranges [c0 + dz L - m, c1 + dz L + m]
-// (dz = -1, 0, 1; L cells per layer, m = nx + 1 covers the rows y +- 1), i.e. in three slot
-// intervals.  Past `cap` slots the row margin m shrinks (the rows y +- 1 partly covered;
-// entries outside are read from HBM).  off(c) = the first slot of cell c.
-template <typename Off>
-__device__ inline PopWin pop_window_core(Off off, int nx, int ny, int ncell, int c0, int c1, int s1, int cap) {
-    const int L = nx * ny;
-    int lo[3], hi[3];
-    auto build = [&](int m) {  // the merged slot intervals for row margin m; returns their total
-        int n = 0, tot = 0;
-        for (int dz = -1; dz <= 1; ++dz) {
-            int a = c0 + dz * L - m, z = c1 + dz * L + m;
-            a = a < 0 ? 0 : a;
-            z = z > ncell - 1 ? ncell - 1 : z;
-            if (a > z) continue;
-            const int sa = off(a), sz = off(z + 1);
-            if (sz <= sa) continue;
-            if (n > 0 && sa <= hi[n - 1]) {
-                hi[n - 1] = max(hi[n - 1], sz);
-            } else {
-                lo[n] = sa;
-                hi[n] = sz;
-                ++n;
-            }
-        }
-        for (int k = 0; k < n; ++k) tot += hi[k] - lo[k];
-        for (int k = n; k < 3; ++k) lo[k] = hi[k] = 0;
-        return tot;
-    };
-    const int m = nx + 1;
-    if (build(m) > cap) {  // the largest margin that fits
-        int good = -1, l = 0, h = m - 1;
-        while (l <= h) {
-            const int mid = (l + h) >> 1;
-            if (build(mid) <= cap) {
-                good = mid;
-                l = mid + 1;
-            } else {
-                h = mid - 1;
-            }
-        }
-        if (good >= 0) {
-            build(good);
-        } else {  // denser than cap even without margins: the block's own cells, clipped around it
-            lo[0] = max(off(c0), s1 + 1 - cap);
-            hi[0] = min(off(c1 + 1), lo[0] + cap);
-            lo[1] = hi[1] = lo[2] = hi[2] = 0;
-        }
-    }
-    PopWin W;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        W.lo[k] = lo[k];
-        W.len[k] = hi[k] - lo[k];
-    }
-    return W;
-}
-
-// the window of block b of flagged structure s at its list build (the fill): from the cells
-// of the block's first and last bead slots and the build's cell offsets
-__device__ inline void pop_store_window(const PopArgs& A, int s, int b, const float4* pos) {
-    PopWin W;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) W.lo[k] = W.len[k] = 0;
-    const int* cell = A.cell + (size_t)s * kPopCells;
-    const int* gn = A.gn + (size_t)s * 8;
-    const float* gp = A.gp + (size_t)s * 8;
-    const int nb[3] = {gn[0], gn[1], gn[2]};
-    const int ncell = pop_ncell(nb);
-    const int nbead = cell[ncell];  // the non-bead run starts after the last cell
-    const int s0 = b * kPopBS, s1 = min(s0 + kPopBS, nbead) - 1;
-    if (s0 <= s1) {
-        const float4 x0 = pos[s0], x1 = pos[s1];
-        const int c0 = pop_cell_index(x0.x, x0.y, x0.z, gp, gp + 3, nb);
-        const int c1 = pop_cell_index(x1.x, x1.y, x1.z, gp, gp + 3, nb);
-        W = pop_window_core([&](int c) { return cell[c]; }, nb[0], nb[1], ncell, c0, c1, s1, kWinCap);
-    }
-    int* wo = A.win + ((size_t)s * A.nbs + b) * 8;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        wo[k] = W.lo[k];
-        wo[3 + k] = W.len[k];
-    }
-}
-
 // The Verlet list of bead slot i of structure s (p0 its position): collected in the
 // thread's LDS row `row` (kPopListRow u16), padded to whole quads with the slot itself,
 // stored as quads to the global list and its length (or kNnbWalk) to nnb.  Returns
@@ -2405,9 +2287,8 @@ __device__ __forceinline__ int pop_fill_slot(const PopArgs& A, const PopList& T,
 // force kernel +9 %).
 //   One block per (flagged structure, slot block): the grid covers every structure of the
 // group and the blocks past *nflag exit (a loop over the flagged structures in a smaller grid
-// costs the kernel 8 VGPRs: 74, 6 waves per SIMD instead of 7).  WIN: thread 0 also stores
-// the block's window (pop_store_window) for the windowed force kernel.
-template <int ROW, bool WIN = false>
+// costs the kernel 8 VGPRs: 74, 6 waves per SIMD instead of 7, profiles/r06_ab).
+template <int ROW>
 __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
     __shared__ uint32_t lrow[kPopBS * ROW / 2];
     const int kb = blockIdx.x / A.nbs;
@@ -2415,7 +2296,6 @@ __global__ void __launch_bounds__(kPopBS) pop_fill_kernel(PopArgs A) {
     const int s = A.flist[kb], blk = blockIdx.x % A.nbs, t = threadIdx.x, i = blk * kPopBS + t;
     const size_t base = (size_t)s * A.cm.ldn;
     const float4* pos = A.buf[A.par[s]].pos + base;
-    if (WIN && t == 0) pop_store_window(A, s, blk, pos);
     if (i >= A.cm.natom) return;
     const float4 p0 = pos[i];
     const PopList T = A.two ? PopList{A.nlo, A.nnbo, A.kqo} : PopList{A.nl, A.nnb, A.kq};
@@ -2528,15 +2408,10 @@ __device__ __noinline__ float4 pop_walk_pairs(const float4* pos, const int* cell
 // (nn_built entries) and is read from there; the slot's bonds are re-indexed from the
 // atom-space adjacency into the new slot order here (written to bent/bdeg for the
 // following steps) and used directly.
-//   WIN: the block's window (W, its positions staged in LDS at wpos) serves every neighbour and
-// bond partner inside it (an LDS read instead of a gather through the texture path); the
-// rest are gathered from HBM.
-template <bool WIN = false>
 __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, size_t base, const float4* pos,
                                                uint32_t fl, float evf, float envf, float& fx, float& fy,
                                                float& fz, const IGM_LDS float2* sbt, bool lds_types,
-                                               const uint32_t* lrow = nullptr, int nn_built = 0,
-                                               const IGM_LDS float4* wpos = nullptr, PopWin W = PopWin{}) {
+                                               const uint32_t* lrow = nullptr, int nn_built = 0) {
     constexpr int U = kPopPairBatch;  // list quads per batch
     const int nsl = A.cm.nslice;
     const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
@@ -2663,7 +2538,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
                     for (int u = 0; u < 2 * U; ++u) pair2(pt[2 * u], pt[2 * u + 1]);
                 }
             };
-            pairs([&](uint32_t j) { return WIN ? pop_wld(wpos, W, rp, j) : pop_ld(rp, j); });
+            pairs([&](uint32_t j) { return pop_ld(rp, j); });
             fx = ax.x + ax.y;
             fy = ay.x + ay.y;
             fz = az.x + az.y;
@@ -2696,7 +2571,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         float2 ct[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            pt[u] = WIN ? pop_wld(wpos, W, rp, et[u] & 0xffffu) : pop_ld(rp, et[u] & 0xffffu);
+            pt[u] = pop_ld(rp, et[u] & 0xffffu);
             ct[u] = lds_types ? sbt[(et[u] >> 16) & 0x7fffu] : bt[(et[u] >> 16) & 0x7fffu];
         }
 #pragma unroll
@@ -2746,13 +2621,13 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 // path): no fill launch, no list or bond re-read on rebuild steps.  Every cross-slot
 // input (the new slot order, cell offsets and positions) was written by the sort and
 // permute kernels before this launch.
-//   WIN: the block's window (A.win, from its last list build) staged in LDS first; every
-// neighbour and bond partner inside it is an LDS read (pop_wld).
-template <bool FUSED, bool WIN = false>
+//   (Block windows staged in LDS, every neighbour inside them an LDS read instead of a
+// gather: round 5 with window-form lists, round 6 with the slot -> window mapping in this
+// kernel -- both slower on config C, profiles/r05_ab and profiles/r06_ab.)
+template <bool FUSED>
 __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(PopArgs A, float evf, float envf, PopStep S) {
     __shared__ double red[kPopBS / 64];
     __shared__ uint32_t lrow[FUSED ? kPopBS * kPopListRow / 2 : 1];
-    __shared__ float4 wpos[WIN ? kWinCap : 1];
     const int lb = pop_block(), s = lb / A.nbs, blk = lb % A.nbs, i = blk * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
     // the build kernels of this step are done (part 1 runs beside them: it leaves the counters)
@@ -2778,19 +2653,6 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
         const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
         for (int q = threadIdx.x; q < (int)ntyp; q += kPopBS) sbt[q] = bt[q];
     }
-    PopWin W;
-    if (WIN) {  // the block's window: three slot intervals, staged back to back (coalesced)
-        const int* wp = A.win + ((size_t)s * A.nbs + blk) * 8;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            W.lo[q] = __builtin_amdgcn_readfirstlane(wp[q]);
-            W.len[q] = __builtin_amdgcn_readfirstlane(wp[3 + q]);
-        }
-        const float4* pb = B.pos + base;
-        const int n0 = W.len[0], n01 = n0 + W.len[1], tot = n01 + W.len[2];
-        for (int q = threadIdx.x; q < tot; q += kPopBS)
-            wpos[q] = pb[q < n0 ? W.lo[0] + q : (q < n01 ? W.lo[1] + q - n0 : W.lo[2] + q - n01)];
-    }
     __syncthreads();
     double ke = 0.0;
     if (i < A.cm.natom) {
@@ -2807,9 +2669,6 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
             else
                 A.nnb[k] = 0;
             pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, (const IGM_LDS float2*)sbt, lds_types, row, nb);
-        } else if (WIN) {
-            pop_slot_force<true>(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, (const IGM_LDS float2*)sbt,
-                                 lds_types, nullptr, 0, (const IGM_LDS float4*)wpos, W);
         } else {
             pop_slot_force(A, s, i, base, B.pos + base, fl, evf, envf, fx, fy, fz, (const IGM_LDS float2*)sbt, lds_types);
         }
@@ -3945,7 +3804,6 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
         V.tid = Q.tid + o;
         V.ctot = Q.ctot + (size_t)s0 * 8;
     }
-    if (Q.win) V.win = Q.win + (size_t)s0 * Q.nbs * 8;
     V.flag[0] = Q.flag[0] + s0;
     V.flag[1] = Q.flag[1] + s0;
     V.oflag[0] = Q.oflag[0] + s0;
@@ -4208,15 +4066,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     // throughput, not by the groups' launch chains, so the shorter chain buys nothing and the
     // second launch and cross-stream events cost.
     const bool early = knob("IGM_POP_EARLY", 0) != 0 && !kPopFused;
-    // block windows (IGM_POP_WIN=1): the fill stores each block's window, the force kernel
-    // stages it in LDS (not with two-level lists: their inner lists are re-filtered, not filled)
-    const bool wmode = knob("IGM_POP_WIN", 0) != 0 && !kPopFused && !Q.two;
-    if (wmode) {
-        void* pw;
-        IGM_TRY(workspace(c, "pop_win", sizeof(int) * 8 * (size_t)S * Q.nbs, &pw));
-        Q.win = (int*)pw;
-    }
-    auto force_kern = wmode ? pop_force_kernel<kPopFused, true> : pop_force_kernel<kPopFused, false>;
+    auto force_kern = pop_force_kernel<kPopFused>;
     IGM_TRY(aux_streams(c, nc + (early ? ng : 0)));
     std::vector<hipEvent_t> ev_int(early ? ng : 0), ev_frc(early ? ng : 0);
     for (int g = 0; g < (early ? ng : 0); ++g) {
@@ -4336,11 +4186,7 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
                             hipLaunchKernelGGL(pop_fill_kernel<kOuterRow>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
                             hipLaunchKernelGGL(pop_refilter_kernel, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
                         } else if (!kPopFused) {
-                            if (wmode)
-                                hipLaunchKernelGGL((pop_fill_kernel<kPopListRow, true>), dim3(ns * Q.nbs), blk, 0, sg,
-                                                   V[g]);
-                            else
-                                hipLaunchKernelGGL(pop_fill_kernel<kPopListRow>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
+                            hipLaunchKernelGGL(pop_fill_kernel<kPopListRow>, dim3(ns * Q.nbs), blk, 0, sg, V[g]);
                         }
                         PopStep s2 = st;
                         s2.part = early ? 2 : 0;
