@@ -17,14 +17,15 @@ TLIM=${TLIM:-900}
 SQ=${SQ:-"SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"}
 (while sleep 50; do date >> $OUT/heartbeat.txt; done) &
 HB=$!
-trap 'kill $HB 2>/dev/null' EXIT
+# the raw rocpd databases exceed what gpurun brings back: removed on every exit, summarised first
+trap 'kill $HB 2>/dev/null; rm -rf $OUT/kt $OUT/fetch $OUT/write $OUT/sqp' EXIT
 for P in ${PASSES:-kt hbm}; do
   case $P in
     kt)
       timeout -k 10 $TLIM rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt -- python3 -u bench.py $ARGS > $OUT/prof_kt.log 2>&1
       rc=$?; echo "kt rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     hbm)
-      for CNT in FETCH_SIZE WRITE_SIZE; do
+      for CNT in ${HBM_COUNTERS:-FETCH_SIZE WRITE_SIZE}; do
         D=$(echo $CNT | cut -d_ -f1 | tr A-Z a-z)
         timeout -s KILL $TLIM rocprofv3 --pmc $CNT -d $OUT/$D -o p -- python3 -u bench.py $ARGS > $OUT/prof_$D.log 2>&1
         rc=$?; echo "pmc $CNT rc=$rc"; [ $rc -eq 0 ] || exit $rc
