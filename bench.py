@@ -17,7 +17,9 @@ config_C block (the metric's own workload, BASELINE.json "200kb diploid pop=1000
 200 kb diploid, pop = --c-total (default 1000) structures STRONG-split over the ranks
 (all 1000 on one GPU; at 8 GPUs the 125-structure shards, the north-star run), Hi-C
 sigma 0.01, full protocol, the A-step over the whole population after one RCCL
-all-gather; c_warmup + c_steps A/M iterations between barriers, max over ranks.
+all-gather; c_warmup warmup A/M iterations at protocol x c_warmup_scale (0.1: RandomInit
+to annealed structures), then c_steps timed full-protocol A/M iterations between barriers,
+max over ranks.
 N=1 only, beside it: the 125-structure shard of config C on frustrated restraints (A-step
 bonds + 700 random long-range contacts per structure), and configurations D and E
 (BASELINE.json configs[3], configs[4]) through one M-step of the 125-structure shard
@@ -70,6 +72,9 @@ def parse():
     ap.add_argument('--c-total', type=int, default=None,
                     help='config C population split over the ranks (default 1000: the metric\'s workload)')
     ap.add_argument('--c-warmup', type=int, default=1, help='warmup A/M iterations of the config C block')
+    ap.add_argument('--c-warmup-scale', type=float, default=0.1,
+                    help='MD steps of the config C warmup iterations x this (they take RandomInit to annealed '
+                         'structures; the timed iterations run the full protocol)')
     ap.add_argument('--c-cpu-scale', type=float, default=0.02,
                     help='protocol scale of the config C CPU-baseline sample (0: skip it)')
     ap.add_argument('--c-shard', type=int, default=125,
@@ -304,9 +309,11 @@ def bench_config_c(args, dev, world, rank, local, backend='nccl'):
             dist.barrier(device_ids=[local]) if backend == 'nccl' else dist.barrier()
         torch.cuda.synchronize(dev)
 
+    it.params = _scaled_prm(inp['prm'], args.c_warmup_scale)
     for w in range(args.c_warmup):
         progress('config C (pop=%d) warmup %d/%d' % (total, w + 1, args.c_warmup))
         it.step()
+    it.params = inp['prm']
     barrier()
     want_cpu = args.c_cpu_scale > 0 and world == 1 and rank == 0
     snap = it.snapshot() if want_cpu else None
@@ -333,7 +340,8 @@ def bench_config_c(args, dev, world, rank, local, backend='nccl'):
         'metric': 'M-step structures/sec + A/M iteration wall-time, 200 kb diploid pop=%d (configs[2]) on %d GPU%s'
                   % (total, world, 's' if world > 1 else ''),
         'value': total * args.c_steps / dt, 'unit': 'structures/s', 'n_gpus': world, 'steps': args.c_steps,
-        'warmup': args.c_warmup, 'ms_per_step': 1000.0 * dt / args.c_steps, 'scaling': 'strong',
+        'warmup': args.c_warmup, 'warmup_protocol_scale': args.c_warmup_scale,
+        'ms_per_step': 1000.0 * dt / args.c_steps, 'scaling': 'strong',
         'config': {'workload': 'C: 200 kb diploid (29 838 beads), Hi-C only, pop=%d, %d structures per GPU, demo '
                                'protocol%s' % (total, per, '' if args.protocol_scale == 1.0 else
                                                ' x%g (NOT the metric)' % args.protocol_scale),
@@ -404,6 +412,18 @@ def _mstep_timed(run, ctx):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return out, dt, {k: ctx.kernel_ms(k) for k in ('anneal', 'cg', 'violations')}
+
+
+def _scaled_prm(prm, scale):
+    """a copy of the M-step parameters with every MD step count x scale (stages and relax runs
+    kept, at least one step each; CG unchanged)"""
+    p = type(prm).from_buffer_copy(prm)
+    if scale != 1.0:
+        for k in range(p.nstages):
+            p.mdsteps[k] = max(1, int(round(p.mdsteps[k] * scale)))
+        if p.relax_steps > 0:
+            p.relax_steps = max(1, int(round(p.relax_steps * scale)))
+    return p
 
 
 def _warm_prm(args, scale=0.1):
