@@ -1452,6 +1452,10 @@ struct PopArgs {
     // bonds of a slot, by buffer parity (as the state): partner slot | type << 16 | lower << 31
     uint32_t* bentb[2];  // (B, nslice, bdmax, 64)
     uint16_t* bdegb[2];  // (B, ldn)
+    // bond pruning (null: off): the slot's bonds that may act before the next list build, in
+    // the same layout and order, and their count -- written by the permute at every build
+    uint32_t* bc;        // (B, nslice, bdmax, 64)
+    uint16_t* bcn;       // (B, ldn)
     // the slot order change of a list build (the sort writes both): new slot -> old slot,
     // old slot -> new slot; the permute moves a slot's state and bonds by them, bond
     // partners re-indexed old slot -> new slot (slot-space reads near the slot, instead
@@ -2147,16 +2151,55 @@ __device__ __forceinline__ void pop_permute_slot(const PopArgs& A, int s, int i)
     const uint32_t* g = A.bentb[p] + ((size_t)s * nsl + (o >> 6)) * A.bdmax * 64 + (o & 63);
     uint32_t* d = A.bentb[q] + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const int* rm = A.remap + base;
-    for (int e0 = 0; e0 < deg; e0 += 4) {  // 4 entries, then their 4 new slots, in flight together
-        uint32_t v[4];
-        int t[4];
+    if (A.bc) {
+        // Bond pruning: between builds every bead stays within skin/2 of its build position
+        // (the integrate's trigger), so a bead-bead distance moves by less than skin.  An
+        // upper bound whose build distance is below r0 - skin (a lower bound: above r0 + skin)
+        // adds exactly 0 until the next build; the candidates keep the entry order, so the
+        // force sums are bitwise those of the whole list.  1 % of the skin covers the f32
+        // rounding; bonds of non-bead atoms (not watched by the trigger) stay candidates.
+        uint32_t* dc = A.bc + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
+        const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
+        const float dsk = 1.01f * A.P.skin;
+        int nc = 0;
+        for (int e0 = 0; e0 < deg; e0 += 4) {  // 4 entries, then their new slots and old positions
+            uint32_t v[4];
+            int t[4];
+            float4 pj[4];
+            float2 ct[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = g[(size_t)min(e0 + u, deg - 1) * 64];
+            for (int u = 0; u < 4; ++u) v[u] = g[(size_t)min(e0 + u, deg - 1) * 64];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) t[u] = rm[v[u] & 0xffffu];
+            for (int u = 0; u < 4; ++u) {
+                t[u] = rm[v[u] & 0xffffu];
+                pj[u] = O.pos[base + (v[u] & 0xffffu)];
+                ct[u] = bt[(v[u] >> 16) & 0x7fffu];
+            }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (e0 + u < deg) d[(size_t)(e0 + u) * 64] = (v[u] & 0xffff0000u) | (uint32_t)t[u];
+            for (int u = 0; u < 4; ++u) {
+                if (e0 + u >= deg) continue;
+                const uint32_t e = (v[u] & 0xffff0000u) | (uint32_t)t[u];
+                d[(size_t)(e0 + u) * 64] = e;
+                const float dx = x.x - pj[u].x, dy = x.y - pj[u].y, dz = x.z - pj[u].z;
+                const float r = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
+                const bool idle = x.w >= 0.0f && pj[u].w >= 0.0f &&
+                                  ((v[u] & kLowerBit) ? r - dsk > ct[u].x : r + dsk < ct[u].x);
+                if (!idle) dc[(size_t)nc++ * 64] = e;
+            }
+        }
+        A.bcn[k] = (uint16_t)nc;
+    } else {
+        for (int e0 = 0; e0 < deg; e0 += 4) {  // 4 entries, then their 4 new slots, in flight together
+            uint32_t v[4];
+            int t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = g[(size_t)min(e0 + u, deg - 1) * 64];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] = rm[v[u] & 0xffffu];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (e0 + u < deg) d[(size_t)(e0 + u) * 64] = (v[u] & 0xffff0000u) | (uint32_t)t[u];
+        }
     }
     A.bdegb[q][k] = (uint16_t)deg;
 }
@@ -2415,7 +2458,8 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     constexpr int U = kPopPairBatch;  // list quads per batch
     const int nsl = A.cm.nslice;
     const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
-    uint32_t* g = A.bentb[A.par[s]] + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
+    // the bonds: the pruned candidates of the last build when the engine keeps them
+    uint32_t* g = (A.bc ? A.bc : A.bentb[A.par[s]]) + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
     const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
     const float4 p0 = pos[i];
@@ -2437,7 +2481,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         ga = A.csr + A.cbase[s] + r0;
         A.bdegb[A.par[s]][base + i] = (uint16_t)deg;
     } else {
-        deg = A.bdegb[A.par[s]][base + i];
+        deg = A.bc ? A.bcn[base + i] : A.bdegb[A.par[s]][base + i];
     }
 #if IGM_POP_PREFETCH
     // Latency: the slot's loads, its first list quad and first bond entries go out in
@@ -2731,7 +2775,7 @@ __global__ void __launch_bounds__(kPopBS) pop_finish_kernel(PopArgs A, PopStep S
 // Tuning diagnostic (IGM_POP_STATS): per run, the Verlet-list and bond-degree shape the
 // force kernel sees after a step -- slots, sum of list lengths (and squares), sum over
 // waves of the wave's longest list in quads (a wave runs to its longest list), walks,
-// bond degrees and the waves' longest.  Never launched in a measured run.
+// bond degrees (the pruned candidates when the engine prunes) and the waves' longest.  Never launched in a measured run.
 __global__ void __launch_bounds__(kPopBS) pop_stats_kernel(PopArgs A, unsigned long long* st) {
     const int lb = pop_block(), s = lb / A.nbs, i = (lb % A.nbs) * kPopBS + threadIdx.x;
     if (s >= A.cm.nstruct) return;
@@ -2740,7 +2784,7 @@ __global__ void __launch_bounds__(kPopBS) pop_stats_kernel(PopArgs A, unsigned l
     int nn = live ? A.nnb[base + i] : 0;
     const int walk = nn == kNnbWalk ? 1 : 0;
     if (walk) nn = 0;
-    const int deg = live ? A.bdegb[A.par[s]][base + i] : 0;
+    const int deg = live ? (A.bc ? A.bcn[base + i] : A.bdegb[A.par[s]][base + i]) : 0;  // (the bonds visited)
     int mq = (nn + 3) >> 2, md = deg;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -2781,7 +2825,8 @@ __global__ void __launch_bounds__(kPopBS) pop_stats_kernel(PopArgs A, unsigned l
     atomicMin(&wlo, lo);
     atomicMax(&whi, hi);
     __syncthreads();
-    const uint32_t* g = A.bentb[A.par[s]] + ((size_t)s * A.cm.nslice + (i >> 6)) * A.bdmax * 64 + (i & 63);
+    const uint32_t* g = (A.bc ? A.bc : A.bentb[A.par[s]]) + ((size_t)s * A.cm.nslice + (i >> 6)) * A.bdmax * 64 +
+                        (i & 63);
     int in = 0;
     for (int e = 0; e < deg; ++e) {
         const int j = (int)(g[(size_t)e * 64] & 0xffffu);
@@ -3797,6 +3842,10 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
         V.bentb[b] = Q.bentb[b] + (size_t)s0 * nsl * Q.bdmax * 64;
         V.bdegb[b] = Q.bdegb[b] + o;
     }
+    if (Q.bc) {
+        V.bc = Q.bc + (size_t)s0 * nsl * Q.bdmax * 64;
+        V.bcn = Q.bcn + o;
+    }
     V.inv = Q.inv + o;
     V.remap = Q.remap + o;
     if (Q.ccnt) {
@@ -3851,10 +3900,12 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
         // HBM of the engine's state, per slot: two parity buffers of (position 16, velocity
         // 12, force 12, atom id 4, slot 4, flags 1), build position 12, Verlet list 8 kq (512
         // B at the default 256 entries -- most of it), list length 2, bonds 2 x 4 bdmax, degree
-        // 2 x 2, slot remaps 8; per structure the cell offsets.  At config C (1000 x 29 839
-        // slots) the lists alone are 15.3 GB.  Checked against the free HBM (plus what this
-        // context's population workspace already holds) before anything is allocated.
-        const size_t per_slot = 2 * (16 + 12 + 12 + 4 + 4 + 1) + 12 + 8 * (size_t)Q.kq + 2 + 8 * (size_t)Q.bdmax + 4 + 8 + 4;
+        // 2 x 2, slot remaps 8, pruned bonds 4 bdmax + 2; per structure the cell offsets.  At
+        // config C (1000 x 29 839 slots) the lists alone are 15.3 GB.  Checked against the free
+        // HBM (plus what this context's population workspace already holds) before anything
+        // is allocated.
+        const size_t per_slot = 2 * (16 + 12 + 12 + 4 + 4 + 1) + 12 + 8 * (size_t)Q.kq + 2 + 12 * (size_t)Q.bdmax + 6 +
+                                8 + 4;
         const size_t need = per_slot * SL + sizeof(int) * (size_t)S * (kPopCells + kPopCntStride);
         size_t held = 0;
         for (const auto& kv : c->ws)
@@ -3941,6 +3992,19 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.bentb[1] = (uint32_t*)pbent + SL * Q.bdmax;
     Q.bdegb[0] = (uint16_t*)pbdeg;
     Q.bdegb[1] = (uint16_t*)pbdeg + SL;
+    // bond pruning at every build (the permute; IGM_POP_BOND_PRUNE=0 turns it off: a test
+    // switch -- the forces are bitwise the same either way).  Not with two-level lists (their
+    // inner builds move the build positions without a permute) nor the fused engine.
+    {
+        const char* e = getenv("IGM_POP_BOND_PRUNE");
+        if ((e ? atoi(e) != 0 : true) && !Q.two && !kPopFused) {
+            void *pbc, *pbcn;
+            IGM_TRY(workspace(c, "pop_bc", sizeof(uint32_t) * SL * Q.bdmax, &pbc));
+            IGM_TRY(workspace(c, "pop_bcn", sizeof(uint16_t) * SL, &pbcn));
+            Q.bc = (uint32_t*)pbc;
+            Q.bcn = (uint16_t*)pbcn;
+        }
+    }
     Q.flag[0] = (int*)pfl;
     Q.flag[1] = (int*)pfl + S;
     Q.flist = (int*)pfli;

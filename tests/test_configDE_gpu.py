@@ -14,12 +14,16 @@ Statistic (tests/mstep_stats.same_population, the one that rejects a 2x bond K o
 2x evfactor in tests/test_mstep_stats.py): two-sample KS at alpha = 1e-3 over 16 vs 16
 structures on E_pair, E_bond, every envelope energy, E_total per bead, the violation
 fraction of every monitored restraint (violation records of both final populations
-scored by the same bit-exact kernel) and the final Temp.  Verlet rebuild counts are
+scored by the same bit-exact kernel) and the final Temp.  The same run without bond
+pruning (IGM_POP_BOND_PRUNE=0) is bitwise the same: SPRITE centroids (not watched by the
+list-build trigger) keep their bonds, DamID and FISH bounds prune like Hi-C's.  Verlet rebuild counts are
 not compared: the GPU's default skin is 0.7 maxrad, the oracle's LAMMPS maxrad.
 Parity of the DamID k < 0 envelope form and of the volumetric force stays UNPINNED
 (no reference output exists): both sides implement the documented
 forms, and this test shows the GPU engine reproduces its own oracle at 200 kb.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -51,6 +55,12 @@ def _run(config):
     try:
         xg, ig, sg = A.run(b, seeds, 0.05, ctx)
         xg2, ig2, _ = A.run(b, seeds, 0.05, ctx)
+        os.environ['IGM_POP_BOND_PRUNE'] = '0'  # every bond at every step: bitwise the same
+        try:
+            xg3, ig3, _ = A.run(b, seeds, 0.05, ctx)
+        finally:
+            del os.environ['IGM_POP_BOND_PRUNE']
+        assert np.array_equal(xg, xg3) and ig.tobytes() == ig3.tobytes(), 'bond pruning changed the run'
         if vol is not None:
             oracle.set_volume(vol)
         xo, io, _ = oracle.mstep_run(b.prm, b.x.copy(), b.radii, b.flags, b.poly, b.ptr, b.bonds, seeds, nthreads=16)
@@ -109,7 +119,6 @@ def test_gpu_200kb_stagewise_matches_oracle(config, heartbeat):
     ModelingStep.py:402-503."""
     import stagewise as SW
     from igm_amd import _lib, assemble as A, volume as V
-    import os
     n, scale = 16, float(os.environ.get('IGM_DE_STAGEWISE_SCALE', '0.1'))
     ctx = _lib.context(0)
     pop = de200.population(config, n, first_sid=900)
