@@ -1350,6 +1350,9 @@ constexpr int kPopRowCap = IGM_POP_ROW_CAP;
 #ifndef IGM_POP_QDEPTH
 #define IGM_POP_QDEPTH 2  // list quads in flight ahead of the one being gathered (2: -0.7 %, profiles/r04_ab)
 #endif
+#ifndef IGM_POP_BOND_BATCH
+#define IGM_POP_BOND_BATCH 4  // force kernel: bond entries (and partner gathers) per batch
+#endif
 #ifndef IGM_POP_FUSED
 // 1: list build + bond re-index inside the force kernel of a rebuild step.  Measured
 // on config C (protocol x0.1, same box): fused -1.8 % anneal alone, but with the
@@ -2489,9 +2492,12 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     // atom's own are clamped into the allocated region and never used).
     uint2 qnext = make_uint2(i * 0x10001u, i * 0x10001u);
     if (!rebuilt) qnext = gl[0];
-    uint32_t et0[4];
+    constexpr int UB = IGM_POP_BOND_BATCH;
+    uint32_t et0[UB];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) et0[u] = rebuilt ? 0u : g[(size_t)min(u, A.bdmax - 1) * 64];
+    for (int u = 0; u < UB; ++u) et0[u] = rebuilt ? 0u : g[(size_t)min(u, A.bdmax - 1) * 64];
+#else
+    constexpr int UB = IGM_POP_BOND_BATCH;
 #endif
     // Two list entries per packed-f32 op.  With t = 1/(r rc) from ONE rsq,
     //   sin(pi r / rc) = sin_rev(r2 t / 2)   and   evf rc sin / (pi r) = evfpi rc2 t sin,
@@ -2588,16 +2594,16 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
             fz = az.x + az.y;
         }
     }
-    for (int k0 = 0; k0 < deg; k0 += 4) {
-        uint32_t et[4];
+    for (int k0 = 0; k0 < deg; k0 += UB) {
+        uint32_t et[UB];
         if (rebuilt) {  // atom-space entries -> slot-space (the permute of the unfused engine)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) et[u] = ga[min(k0 + u, deg - 1)];
-            int sv[4];
+            for (int u = 0; u < UB; ++u) et[u] = ga[min(k0 + u, deg - 1)];
+            int sv[UB];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) sv[u] = sl[et[u] & 0xffffu];
+            for (int u = 0; u < UB; ++u) sv[u] = sl[et[u] & 0xffffu];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < UB; ++u) {
                 et[u] = (et[u] & 0xffff0000u) | (uint32_t)sv[u];
                 if (k0 + u < deg) g[(size_t)(k0 + u) * 64] = et[u];
             }
@@ -2605,21 +2611,21 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
 #if IGM_POP_PREFETCH
             if (k0 == 0) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) et[u] = u < deg ? et0[u] : et0[0];  // (past deg: a valid entry)
+                for (int u = 0; u < UB; ++u) et[u] = u < deg ? et0[u] : et0[0];  // (past deg: a valid entry)
             } else
 #endif
 #pragma unroll
-            for (int u = 0; u < 4; ++u) et[u] = g[(size_t)min(k0 + u, deg - 1) * 64];
+            for (int u = 0; u < UB; ++u) et[u] = g[(size_t)min(k0 + u, deg - 1) * 64];
         }
-        float4 pt[4];
-        float2 ct[4];
+        float4 pt[UB];
+        float2 ct[UB];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < UB; ++u) {
             pt[u] = pop_ld(rp, et[u] & 0xffffu);
             ct[u] = lds_types ? sbt[(et[u] >> 16) & 0x7fffu] : bt[(et[u] >> 16) & 0x7fffu];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) bond(pt[u], ct[u], et[u], k0 + u < deg);
+        for (int u = 0; u < UB; ++u) bond(pt[u], ct[u], et[u], k0 + u < deg);
     }
     fx += bfx;
     fy += bfy;
