@@ -1459,6 +1459,9 @@ struct PopArgs {
     // the same layout and order, and their count -- written by the permute at every build
     uint32_t* bc;        // (B, nslice, bdmax, 64)
     uint16_t* bcn;       // (B, ldn)
+    int* bpr;            // (B) the structure's last build pruned (1) or kept every bond (0)
+    int* bage;           // (B) steps its lists have served since their build (the force kernel counts)
+    int prune_age;       // a build prunes when the lists it replaces served at least this many steps
     // the slot order change of a list build (the sort writes both): new slot -> old slot,
     // old slot -> new slot; the permute moves a slot's state and bonds by them, bond
     // partners re-indexed old slot -> new slot (slot-space reads near the slot, instead
@@ -2154,7 +2157,9 @@ __device__ __forceinline__ void pop_permute_slot(const PopArgs& A, int s, int i)
     const uint32_t* g = A.bentb[p] + ((size_t)s * nsl + (o >> 6)) * A.bdmax * 64 + (o & 63);
     uint32_t* d = A.bentb[q] + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const int* rm = A.remap + base;
-    if (A.bc) {
+    const bool prune = A.bc && A.bage[s] >= A.prune_age;
+    if (A.bc && i == 0) A.bpr[s] = prune ? 1 : 0;
+    if (prune) {
         // Bond pruning: between builds every bead stays within skin/2 of its build position
         // (the integrate's trigger), so a bead-bead distance moves by less than skin.  An
         // upper bound whose build distance is below r0 - skin (a lower bound: above r0 + skin)
@@ -2462,7 +2467,8 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
     const int nsl = A.cm.nslice;
     const uint2* gl = A.nl + ((size_t)s * nsl + (i >> 6)) * A.kq * 64 + (i & 63);
     // the bonds: the pruned candidates of the last build when the engine keeps them
-    uint32_t* g = (A.bc ? A.bc : A.bentb[A.par[s]]) + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
+    const bool pruned = A.bc && A.bpr[s];
+    uint32_t* g = (pruned ? A.bc : A.bentb[A.par[s]]) + ((size_t)s * nsl + (i >> 6)) * A.bdmax * 64 + (i & 63);
     const float2* bt = A.cm.bonds.types + A.cm.bonds.tbase[s];
     const __amdgpu_buffer_rsrc_t rp = pop_rsrc(pos, A.cm.natom);
     const float4 p0 = pos[i];
@@ -2484,7 +2490,7 @@ __device__ __forceinline__ void pop_slot_force(const PopArgs& A, int s, int i, s
         ga = A.csr + A.cbase[s] + r0;
         A.bdegb[A.par[s]][base + i] = (uint16_t)deg;
     } else {
-        deg = A.bc ? A.bcn[base + i] : A.bdegb[A.par[s]][base + i];
+        deg = pruned ? A.bcn[base + i] : A.bdegb[A.par[s]][base + i];
     }
 #if IGM_POP_PREFETCH
     // Latency: the slot's loads, its first list quad and first bond entries go out in
@@ -2689,6 +2695,7 @@ __global__ void __launch_bounds__(kPopBS, IGM_POP_FORCE_OCC) pop_force_kernel(Po
     if ((S.part == 1 && rebuilt) || (S.part == 2 && !rebuilt)) return;  // (block-uniform)
     if (i == 0) {
         A.nrebuild[s] += rebuilt ? 1 : 0;
+        if (A.bc) A.bage[s] = rebuilt ? 0 : A.bage[s] + 1;
         A.flag[S.fp ^ 1][s] = 0;  // the next step's flags start clear
         A.oflag[S.fp ^ 1][s] = 0;
     }
@@ -2790,7 +2797,8 @@ __global__ void __launch_bounds__(kPopBS) pop_stats_kernel(PopArgs A, unsigned l
     int nn = live ? A.nnb[base + i] : 0;
     const int walk = nn == kNnbWalk ? 1 : 0;
     if (walk) nn = 0;
-    const int deg = live ? (A.bc ? A.bcn[base + i] : A.bdegb[A.par[s]][base + i]) : 0;  // (the bonds visited)
+    const bool pruned = A.bc && A.bpr[s];
+    const int deg = live ? (pruned ? A.bcn[base + i] : A.bdegb[A.par[s]][base + i]) : 0;  // (the bonds visited)
     int mq = (nn + 3) >> 2, md = deg;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -2831,7 +2839,7 @@ __global__ void __launch_bounds__(kPopBS) pop_stats_kernel(PopArgs A, unsigned l
     atomicMin(&wlo, lo);
     atomicMax(&whi, hi);
     __syncthreads();
-    const uint32_t* g = (A.bc ? A.bc : A.bentb[A.par[s]]) + ((size_t)s * A.cm.nslice + (i >> 6)) * A.bdmax * 64 +
+    const uint32_t* g = (pruned ? A.bc : A.bentb[A.par[s]]) + ((size_t)s * A.cm.nslice + (i >> 6)) * A.bdmax * 64 +
                         (i & 63);
     int in = 0;
     for (int e = 0; e < deg; ++e) {
@@ -3851,6 +3859,8 @@ PopArgs pop_view(const PopArgs& Q, int s0, int ns, int g) {
     if (Q.bc) {
         V.bc = Q.bc + (size_t)s0 * nsl * Q.bdmax * 64;
         V.bcn = Q.bcn + o;
+        V.bpr = Q.bpr + s0;
+        V.bage = Q.bage + s0;
     }
     V.inv = Q.inv + o;
     V.remap = Q.remap + o;
@@ -3998,17 +4008,28 @@ int run_anneal_pop(igm_ctx* c, const Prepared& pr, const AnnealArgs& A) {
     Q.bentb[1] = (uint32_t*)pbent + SL * Q.bdmax;
     Q.bdegb[0] = (uint16_t*)pbdeg;
     Q.bdegb[1] = (uint16_t*)pbdeg + SL;
-    // bond pruning at every build (the permute; IGM_POP_BOND_PRUNE=0 turns it off: a test
+    // bond pruning at list builds (the permute; IGM_POP_BOND_PRUNE=0 turns it off: a test
     // switch -- the forces are bitwise the same either way).  Not with two-level lists (their
     // inner builds move the build positions without a permute) nor the fused engine.
     {
         const char* e = getenv("IGM_POP_BOND_PRUNE");
         if ((e ? atoi(e) != 0 : true) && !Q.two && !kPopFused) {
-            void *pbc, *pbcn;
+            void *pbc, *pbcn, *pbpr;
             IGM_TRY(workspace(c, "pop_bc", sizeof(uint32_t) * SL * Q.bdmax, &pbc));
             IGM_TRY(workspace(c, "pop_bcn", sizeof(uint16_t) * SL, &pbcn));
+            IGM_TRY(workspace(c, "pop_bpr", sizeof(int) * 2 * (size_t)S, &pbpr));
+            // ages start large: the first build prunes
+            IGM_HIP_CHECK(c, hipMemsetAsync(pbpr, 0x3f, sizeof(int) * 2 * (size_t)S, c->stream));
             Q.bc = (uint32_t*)pbc;
             Q.bcn = (uint16_t*)pbcn;
+            Q.bpr = (int*)pbpr;
+            Q.bage = (int*)pbpr + S;
+            // Prune only at builds whose replaced lists served >= 6 steps (IGM_POP_PRUNE_AGE, tuning):
+            // a structure rebuilding every few steps pays the permute's partner gathers and saves
+            // little (measured on the 125-structure shard, full protocol, same box: always -1.4 %,
+            // age >= 6 -3.2 % against no pruning; frustrated -0.9 %, config E +0.4 %; profiles/r06_ab)
+            const char* ea = getenv("IGM_POP_PRUNE_AGE");
+            Q.prune_age = ea ? atoi(ea) : 6;
         }
     }
     Q.flag[0] = (int*)pfl;

@@ -219,7 +219,8 @@ def test_gpu_200kb_build_variants_bitwise_equal(ms, model200):
     is the engine with the forces of the structures not rebuilt at a step running ahead of
     the list builds on a second stream (IGM_POP_EARLY=1), and the engine without bond
     pruning (IGM_POP_BOND_PRUNE=0: every bond visited at every step, the pruned ones adding
-    exactly 0)."""
+    exactly 0) or pruning at every build (IGM_POP_PRUNE_AGE=0; default: builds whose lists
+    served >= 6 steps)."""
     atoms, poly, prm, ptr, sb, x = model200
     n = 6
     x6 = np.concatenate([x] * 3)
@@ -241,9 +242,10 @@ def test_gpu_200kb_build_variants_bitwise_equal(ms, model200):
     xr, ir = _with_env({'IGM_POP_SORT': '1'}, run)
     xe, ie = _with_env({'IGM_POP_EARLY': '1'}, run)
     xp, ip = _with_env({'IGM_POP_BOND_PRUNE': '0'}, run)
+    xa, ia = _with_env({'IGM_POP_PRUNE_AGE': '0'}, run)
     assert np.all(is_['nrebuild'] > 10)  # many list builds
     runs = {'lds sort': (xl, il), 'split sort, 1 build slot, 3 groups': (x1, i1), 'split sort rerun': (xr, ir),
-            'early forces': (xe, ie), 'no bond pruning': (xp, ip)}
+            'early forces': (xe, ie), 'no bond pruning': (xp, ip), 'pruning at every build': (xa, ia)}
     bad = [k for k, (xo, io) in runs.items() if not (np.array_equal(xs, xo) and is_.tobytes() == io.tobytes())]
     assert not bad, bad
 
